@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CRC32C GiB/s over device-resident 4 KiB SSTable blocks.
+
+Workload (BASELINE.json configs[1]): 1,048,576 blocks x
+4096 B = 4 GiB per GPU, stride 4096, bytes from the on-device splitmix64
+stream (seed 0x5EED0000 + rank), resident in HBM before timing starts.  One
+*step* = one lsbm_crc32c_fixed_dev launch over the whole batch (crc32c::Value
+of every block, util/crc32c.cc:286-329).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+With N > 1 it is launched by torch.distributed.run, one process per GPU; each
+rank checksums its own 1M-block shard (weak scaling, no data-path collective:
+blocks are independent).  Timing: W untimed steps, barrier + synchronize, K
+steps between HIP events on the launch stream, barrier + synchronize, max over
+ranks.  Rank 0 prints ONE JSON line.
+
+Extra fields: roofline (achieved algorithmic GB/s of the dominant kernel vs the
+8 TB/s HBM peak), cpu_baseline (the reference CPU CRC on the host cores, rank 0
+at N=1 only, bounded sample), stream_read (a plain 16-B-per-lane read of the
+same buffer: the measured read ceiling).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "CRC32C GiB/s over device-resident 4 KiB SSTable blocks (1 GPU); % HBM peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec, MI355X_MICROARCH.md "Chip-level parameters"
+BLOCK = 4096
+NBLOCKS = 1 << 20
+SEED = 0x5EED0000
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--blocks", type=int, default=NBLOCKS, help=argparse.SUPPRESS)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="aggregate CPU-seconds for the cpu_baseline sample")
+    return p.parse_args()
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from a committed rocprofv3 PMC pass, if any."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
+    """Time the CPU CRC-32C on the host: the reference's own util/crc32c.cc
+    (oracle/_ref, built from /root/reference) when present, else the oracle's
+    plain-C restatement of it.  Also cross-checks the GPU results on the sample."""
+    import subprocess
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_crc32c.so")
+    port = os.path.join(REPO, "oracle", "liboracle_crc32c.so")
+    if os.path.exists(ref):
+        lib, fn, kind = ctypes.CDLL(ref), "ref_batch_fixed_mt", "reference"
+    else:
+        if not os.path.exists(port):
+            subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL)
+        lib, fn, kind = ctypes.CDLL(port), "oracle_batch_fixed_mt", "port"
+    f = getattr(lib, fn)
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                  ctypes.c_void_p, ctypes.c_int]
+    oracle = ctypes.CDLL(port if os.path.exists(port) else ref)
+    # host bytes of the first `sample_blocks` blocks of rank 0's buffer
+    from tests.golden.splitmix import stream_bytes
+    data = stream_bytes(SEED, 0, sample_blocks * BLOCK)
+    out = np.empty(sample_blocks, dtype=np.uint32)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    f(data.ctypes.data, BLOCK, BLOCK, sample_blocks, out.ctypes.data, threads)  # warm
+    mismatches = int(np.count_nonzero(out != gpu_crcs[:sample_blocks]))
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        f(data.ctypes.data, BLOCK, BLOCK, sample_blocks, out.ctypes.data, threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el * threads >= cpu_seconds or el > 30:
+            break
+    gib = passes * sample_blocks * BLOCK / 2**30
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    del oracle
+    return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{passes} passes x {sample_blocks} x {BLOCK} B blocks (first blocks of "
+                      f"the rank-0 buffer, host copy), crc32c::Value slice-by-4, "
+                      f"{threads} pthreads, {el:.1f} s wall; {cpu_model}",
+            "gpu_mismatches_on_sample": mismatches}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from lsbm_amd import engine
+    engine.init(local)
+    n = args.blocks
+    data = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(data, SEED + rank)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        engine.crc32c_fixed(data, BLOCK, BLOCK, n, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1)  # K launches on the launch stream
+    t_local = max(wall, kern_ms / 1e3)
+    t = torch.tensor([t_local], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+
+    # stream-read ceiling on the same buffer (same stream, same events)
+    sink = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        engine.stream_read(data, sink, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        engine.stream_read(data, sink, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    stream_gbps = 10 * n * BLOCK / (e0.elapsed_time(e1) / 1e3) / 1e9
+
+    total_bytes = n * BLOCK * world * args.steps
+    value = total_bytes / t_max / 2**30
+    per_launch_s = kern_ms / 1e3 / args.steps
+    achieved = n * BLOCK / per_launch_s / 1e9
+    workload = f"{n} x {BLOCK} B device-resident blocks per GPU, batched crc32c::Value"
+    traffic = load_traffic(workload)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gpu_crcs = out.cpu().numpy().view(np.uint32)
+        cpu = cpu_baseline(min(n, 65536), gpu_crcs, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: on-device splitmix64 bytes (seed 0x{SEED:X} + rank), "
+                    "resident in HBM before timing",
+            "config": {"workload": workload, "blocks_per_gpu": n, "block_bytes": BLOCK,
+                       "stride": BLOCK, "baseline_config": "BASELINE.json configs[1]",
+                       "parallelism": f"{world} independent shards, no collective"},
+            "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBPS, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": "crc32c_fixed_kernel<false,32>",
+                         "algorithmic_bytes_per_launch": n * BLOCK,
+                         "avg_launch_ms": round(per_launch_s * 1e3, 4)},
+            "stream_read": {"GBps": round(stream_gbps, 1),
+                            "crc_frac_of_stream_read": round(achieved / stream_gbps, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,117 @@
+/*
+ * lsbm_crc32c.h -- C ABI of the MI355X (gfx950) batched CRC-32C engine for
+ * lsbm's block checksums.  Implemented by lsbm_amd/liblsbm_crc32c.so.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, never throws
+ * and never aborts.  Status codes are the LSBM_* values below (0 = ok).
+ * Device (`_dev`) entry points take device pointers and an explicit HIP stream
+ * (`void* stream` is a hipStream_t; NULL = the legacy default stream); they
+ * only enqueue work, never synchronise, and may be captured into a hipGraph
+ * once the device has been initialised with lsbm_crc32c_init().
+ * They are thread-safe: per-device tables are built once (std::call_once) and
+ * are read-only afterwards; callers serialise through their own streams.
+ *
+ * Reference interfaces replaced (lsbm = tengdj/lsbm, a LevelDB 1.15 fork):
+ *   util/crc32c.h:17-40      crc32c::Extend / Value / Mask / Unmask
+ *                            -> lsbm_crc32c_extend/_value/_mask/_unmask (scalar)
+ *                               and include/util/crc32c.h (same C++ API)
+ *   util/crc32c.cc:286-329   the per-block Extend loop, batched
+ *                            -> lsbm_crc32c_fixed_dev / lsbm_crc32c_batch_dev
+ *   table/table_builder.cc:237-255  TableBuilder::WriteRawBlock trailer seal
+ *                            -> lsbm_sst_seal_dev
+ *   table/format.cc:95-103   ReadBlock's verify_checksums compare
+ *                            -> lsbm_sst_verify_dev
+ *   table/format.h:84        kBlockTrailerSize = 5 -> LSBM_BLOCK_TRAILER_SIZE
+ */
+#ifndef LSBM_CRC32C_H_
+#define LSBM_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define LSBM_OK 0
+#define LSBM_ERR_INVALID (-1)     /* bad argument (null pointer, size, flags) */
+#define LSBM_ERR_NO_DEVICE (-2)   /* no HIP device / bad device ordinal */
+#define LSBM_ERR_HIP (-3)         /* a HIP runtime call failed */
+#define LSBM_ERR_NOMEM (-4)       /* device or pinned allocation failed */
+#define LSBM_ERR_CORRUPTION (-5)  /* verify found >= 1 mismatching block */
+
+/* ---- flags ---- */
+#define LSBM_CRC32C_MASKED 0x1u /* out = Mask(crc) (util/crc32c.h:31-34) */
+
+#define LSBM_CRC32C_MASK_DELTA 0xa282ead8u /* util/crc32c.h:24 kMaskDelta */
+#define LSBM_BLOCK_TRAILER_SIZE 5          /* table/format.h:84 */
+
+/* ---- scalar API: identical results to util/crc32c.{h,cc}; host CPU ---- */
+uint32_t lsbm_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
+uint32_t lsbm_crc32c_value(const char* data, size_t n);
+uint32_t lsbm_crc32c_mask(uint32_t crc);
+uint32_t lsbm_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- engine ---- */
+/* Builds the per-device tables (idempotent, thread-safe).  Optional: every
+ * _dev call initialises lazily, but graph capture needs it done beforehand. */
+int lsbm_crc32c_init(int device);
+/* Library version string and the last HIP error text seen on this thread. */
+const char* lsbm_crc32c_version(void);
+const char* lsbm_crc32c_last_error(void);
+
+/* Fixed-stride batch: block i = d_base[i*stride, i*stride + len).
+ * out[i] = Extend(init ? init[i] : 0, block i, len), Mask()ed if flags has
+ * LSBM_CRC32C_MASKED.  d_init may be NULL (crc32c::Value).  Any stride/len;
+ * 16-B aligned base, stride % 16 == 0 and len % 128 == 0 take the fast path. */
+int lsbm_crc32c_fixed_dev(const void* d_base, uint64_t stride, uint64_t len, uint64_t n_blocks,
+                          const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
+
+/* Ragged batch: block i = d_base[offsets[i], offsets[i+1]) (d_offsets has
+ * n_blocks+1 entries, non-decreasing not required; any alignment). */
+int lsbm_crc32c_batch_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks,
+                          const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
+
+/* Ragged verify: d_ok[i] = (crc of block i == d_expect[i]) where d_expect holds
+ * masked values if flags has LSBM_CRC32C_MASKED.  If d_nbad != NULL the
+ * number of mismatches is ADDED to *d_nbad (caller zeroes it). */
+int lsbm_crc32c_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks,
+                           const uint32_t* d_init, const uint32_t* d_expect, uint8_t* d_ok,
+                           uint32_t* d_nbad, uint32_t flags, void* stream);
+
+/* ---- SSTable block trailers over a device-resident file image ----
+ * d_handles holds n_blocks BlockHandles as {offset, size} uint64 pairs
+ * (table/format.h:22-50).  The block occupies file[offset, offset+size) and its
+ * 5-byte trailer [type u8][Mask(crc32c(block || type)) LE32] follows it. */
+/* WriteRawBlock (table/table_builder.cc:237-255): write each trailer, with
+ * type = d_types[i] (CompressionType, include/leveldb/options.h:24-29). */
+int lsbm_sst_seal_dev(uint8_t* d_file, const uint64_t* d_handles, const uint8_t* d_types,
+                      uint64_t n_blocks, void* stream);
+/* ReadBlock verify (table/format.cc:95-103): d_ok[i] = 1 iff
+ * Unmask(DecodeFixed32(trailer+1)) == Value(block || type); mismatches are
+ * added to *d_nbad when non-NULL. */
+int lsbm_sst_verify_dev(const uint8_t* d_file, const uint64_t* d_handles, uint64_t n_blocks,
+                        uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+
+/* ---- host-staged batch (blocks start and end in host memory) ----
+ * Same contract as lsbm_crc32c_batch_dev but every pointer is a host pointer
+ * (pageable or pinned).  Bytes are streamed through pinned staging buffers
+ * with hipMemcpyAsync overlapped with the kernel; blocks on `device`.
+ * Synchronous: returns when h_out is filled. */
+int lsbm_crc32c_batch_host(int device, const void* h_base, const uint64_t* h_offsets,
+                           uint64_t n_blocks, const uint32_t* h_init, uint32_t* h_out,
+                           uint32_t flags);
+
+/* ---- benchmark / diagnostic helpers (not on the checksum path) ---- */
+/* d_buf[k] = byte k of the splitmix64 stream `seed`. */
+int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream);
+/* Reads nbytes (16-B aligned, multiple of 16) once with 16-B loads and writes
+ * one xor word per workgroup into d_sink[0..1023]: the stream-read ceiling. */
+int lsbm_stream_read_dev(const void* d_buf, uint64_t nbytes, uint32_t* d_sink, void* stream);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* LSBM_CRC32C_H_ */

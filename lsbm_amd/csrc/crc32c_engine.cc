@@ -1,0 +1,464 @@
+// crc32c_engine.cc -- the C ABI of include/lsbm_crc32c.h (host side).
+//
+// Owns the per-device tables (built once with std::call_once, then read-only),
+// validates arguments, picks the kernel, and runs the host-staged pipeline.
+// Never throws, never aborts, never computes a batch on the CPU: without a
+// usable HIP device every batch entry point returns LSBM_ERR_NO_DEVICE.
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/lsbm_crc32c.h"
+#include "crc32c_types.h"
+#include "gf2.h"
+
+namespace lsbm {
+
+// launchers (crc32c_kernels.hip)
+hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uint64_t n_blocks,
+                        const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
+                        const DevConsts* dc, int grid, hipStream_t stream);
+hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
+hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, int grid, hipStream_t stream);
+hipError_t launch_stream_read(const void* buf, uint64_t nbytes, uint32_t* sink, int grid,
+                              hipStream_t stream);
+
+namespace {
+
+thread_local char t_last_error[256] = "";
+
+int fail_hip(hipError_t e, const char* what) {
+  snprintf(t_last_error, sizeof(t_last_error), "%s: %s", what, hipGetErrorString(e));
+  return LSBM_ERR_HIP;
+}
+int fail(int code, const char* what) {
+  snprintf(t_last_error, sizeof(t_last_error), "%s", what);
+  return code;
+}
+
+constexpr int kMaxDevices = 64;
+
+struct DeviceState {
+  std::once_flag once;
+  int status = LSBM_ERR_NO_DEVICE;
+  DevConsts* d_consts = nullptr;
+  int num_cus = 0;
+};
+DeviceState g_dev[kMaxDevices];
+
+void build_consts(DevConsts* c) {
+  gf2::byte_tables(gf2::byte_pow(kRowBytes), c->row_byte);
+  {
+    uint32_t tmp[1024];
+    gf2::byte_tables(gf2::byte_pow(1), tmp);
+    memcpy(c->t0, tmp, sizeof(c->t0));  // M(b << 0) = A(b) = table0_[b]
+  }
+  gf2::Mat p = gf2::byte_pow(1);
+  for (int k = 0; k < 64; k++) {
+    gf2::nibble_tables(p, c->pow_nib[k]);
+    p = gf2::mul(p, p);
+  }
+  for (int z = 0; z < 128; z++) gf2::nibble_tables(gf2::byte_pow(-z), c->neg_nib[z]);
+  gf2::nibble_tables(gf2::byte_pow(-4), c->neg4_nib);
+}
+
+void init_device(int dev, DeviceState* st) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || dev < 0 || dev >= count) {
+    st->status = LSBM_ERR_NO_DEVICE;
+    return;
+  }
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) {
+    st->status = fail_hip(e, "hipSetDevice");
+    return;
+  }
+  int cus = 0;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess || cus <= 0) cus = 256;
+  DevConsts* h = new (std::nothrow) DevConsts;
+  if (!h) {
+    st->status = fail(LSBM_ERR_NOMEM, "host alloc");
+    hipSetDevice(prev);
+    return;
+  }
+  build_consts(h);
+  DevConsts* d = nullptr;
+  e = hipMalloc(&d, sizeof(DevConsts));
+  if (e == hipSuccess) e = hipMemcpy(d, h, sizeof(DevConsts), hipMemcpyHostToDevice);
+  delete h;
+  if (e != hipSuccess) {
+    st->status = fail_hip(e, "device tables");
+    if (d) hipFree(d);
+    hipSetDevice(prev);
+    return;
+  }
+  st->d_consts = d;
+  st->num_cus = cus;
+  st->status = LSBM_OK;
+  hipSetDevice(prev);
+}
+
+int ensure_device(int dev, DeviceState** out) {
+  if (dev < 0 || dev >= kMaxDevices) return fail(LSBM_ERR_NO_DEVICE, "bad device ordinal");
+  DeviceState* st = &g_dev[dev];
+  std::call_once(st->once, init_device, dev, st);
+  if (st->status != LSBM_OK) return st->status;
+  *out = st;
+  return LSBM_OK;
+}
+
+int current_device(DeviceState** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail(LSBM_ERR_NO_DEVICE, "no current HIP device");
+  return ensure_device(dev, out);
+}
+
+int grid_for(const DeviceState* st, uint64_t n_blocks) {
+  const uint64_t groups = (n_blocks + 7) / 8;
+  const uint64_t wgs = (groups + kWavesPerWg - 1) / kWavesPerWg;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(wgs, (uint64_t)st->num_cus));
+}
+
+int run_ragged(RaggedArgs a, hipStream_t stream) {
+  DeviceState* st = nullptr;
+  int rc = current_device(&st);
+  if (rc != LSBM_OK) return rc;
+  if (a.n == 0) return LSBM_OK;
+  a.dc = st->d_consts;
+  hipError_t e = launch_ragged(a, grid_for(st, a.n), stream);
+  return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_ragged_kernel");
+}
+
+// ---- host-staged pipeline ----
+struct Slot {
+  uint8_t* h_data = nullptr;  // pinned
+  uint64_t* h_off = nullptr;  // pinned
+  uint32_t* h_init = nullptr;
+  uint32_t* h_out = nullptr;
+  uint8_t* d_data = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_init = nullptr;
+  uint32_t* d_out = nullptr;
+  uint64_t cap_bytes = 0, cap_blocks = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  // pending chunk
+  bool busy = false;
+  uint64_t first = 0, count = 0;
+};
+
+struct Staging {
+  std::mutex mu;
+  bool ready = false;
+  Slot slot[3];
+};
+Staging g_staging[kMaxDevices];
+
+void free_slot_buffers(Slot& s) {
+  if (s.h_data) hipHostFree(s.h_data);
+  if (s.h_off) hipHostFree(s.h_off);
+  if (s.h_init) hipHostFree(s.h_init);
+  if (s.h_out) hipHostFree(s.h_out);
+  if (s.d_data) hipFree(s.d_data);
+  if (s.d_off) hipFree(s.d_off);
+  if (s.d_init) hipFree(s.d_init);
+  if (s.d_out) hipFree(s.d_out);
+  s.h_data = nullptr; s.h_off = nullptr; s.h_init = nullptr; s.h_out = nullptr;
+  s.d_data = nullptr; s.d_off = nullptr; s.d_init = nullptr; s.d_out = nullptr;
+  s.cap_bytes = s.cap_blocks = 0;
+}
+
+hipError_t reserve_slot(Slot& s, uint64_t bytes, uint64_t blocks) {
+  if (!s.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  if (bytes <= s.cap_bytes && blocks <= s.cap_blocks) return hipSuccess;
+  free_slot_buffers(s);
+  bytes = std::max<uint64_t>(bytes, 64ull << 20);
+  blocks = std::max<uint64_t>(blocks, 1ull << 16);
+  hipError_t e;
+  if ((e = hipHostMalloc((void**)&s.h_data, bytes, hipHostMallocDefault)) != hipSuccess) return e;
+  if ((e = hipHostMalloc((void**)&s.h_off, (blocks + 1) * 8, hipHostMallocDefault)) != hipSuccess)
+    return e;
+  if ((e = hipHostMalloc((void**)&s.h_init, blocks * 4, hipHostMallocDefault)) != hipSuccess)
+    return e;
+  if ((e = hipHostMalloc((void**)&s.h_out, blocks * 4, hipHostMallocDefault)) != hipSuccess)
+    return e;
+  if ((e = hipMalloc(&s.d_data, bytes)) != hipSuccess) return e;
+  if ((e = hipMalloc(&s.d_off, (blocks + 1) * 8)) != hipSuccess) return e;
+  if ((e = hipMalloc(&s.d_init, blocks * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&s.d_out, blocks * 4)) != hipSuccess) return e;
+  s.cap_bytes = bytes;
+  s.cap_blocks = blocks;
+  return hipSuccess;
+}
+
+}  // namespace
+}  // namespace lsbm
+
+using namespace lsbm;
+
+extern "C" {
+
+__attribute__((visibility("default"))) const char* lsbm_crc32c_version(void) {
+  return "lsbm-crc32c-mi355x 0.1 (gfx950)";
+}
+
+__attribute__((visibility("default"))) const char* lsbm_crc32c_last_error(void) {
+  return t_last_error;
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_init(int device) {
+  DeviceState* st = nullptr;
+  return ensure_device(device, &st);
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
+    const void* d_base, uint64_t stride, uint64_t len, uint64_t n_blocks, const uint32_t* d_init,
+    uint32_t* d_out, uint32_t flags, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_base || !d_out) return fail(LSBM_ERR_INVALID, "null pointer");
+  if (flags & ~LSBM_CRC32C_MASKED) return fail(LSBM_ERR_INVALID, "unknown flags");
+  DeviceState* st = nullptr;
+  int rc = current_device(&st);
+  if (rc != LSBM_OK) return rc;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(d_base);
+  const bool fast = (b % 16 == 0) && (stride % 16 == 0) && len >= kRowBytes &&
+                    (len % kRowBytes == 0) && (len / kRowBytes) <= 0xffffffffull;
+  if (fast) {
+    const gf2::Mat an = gf2::byte_pow((int64_t)len);
+    const uint32_t k_value = gf2::apply(an, 0xffffffffu) ^ 0xffffffffu;
+    hipError_t e = launch_fixed(static_cast<const uint8_t*>(d_base), stride,
+                                (uint32_t)(len / kRowBytes), n_blocks, d_init, d_out, flags,
+                                k_value, st->d_consts, grid_for(st, n_blocks),
+                                static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_fixed_kernel");
+  }
+  // Any other geometry: the ragged kernel with fixed-stride extents.
+  RaggedArgs a = {};
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.stride = stride;
+  a.len = len;
+  a.extents = kExtFixed;
+  a.n = n_blocks;
+  a.init = d_init;
+  a.out = d_out;
+  a.flags = flags;
+  a.mode = kModeOut;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_batch_dev(
+    const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks, const uint32_t* d_init,
+    uint32_t* d_out, uint32_t flags, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_base || !d_offsets || !d_out) return fail(LSBM_ERR_INVALID, "null pointer");
+  if (flags & ~LSBM_CRC32C_MASKED) return fail(LSBM_ERR_INVALID, "unknown flags");
+  RaggedArgs a = {};
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.offsets = d_offsets;
+  a.n = n_blocks;
+  a.init = d_init;
+  a.out = d_out;
+  a.flags = flags;
+  a.mode = kModeOut;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_verify_dev(
+    const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks, const uint32_t* d_init,
+    const uint32_t* d_expect, uint8_t* d_ok, uint32_t* d_nbad, uint32_t flags, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_base || !d_offsets || !d_expect || !d_ok) return fail(LSBM_ERR_INVALID, "null pointer");
+  if (flags & ~LSBM_CRC32C_MASKED) return fail(LSBM_ERR_INVALID, "unknown flags");
+  RaggedArgs a = {};
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.offsets = d_offsets;
+  a.n = n_blocks;
+  a.init = d_init;
+  a.expect = d_expect;
+  a.ok = d_ok;
+  a.nbad = d_nbad;
+  a.flags = flags;
+  a.mode = kModeVerify;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file,
+                                                             const uint64_t* d_handles,
+                                                             const uint8_t* d_types,
+                                                             uint64_t n_blocks, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_file || !d_handles || !d_types) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_file;
+  a.file = d_file;
+  a.handles = d_handles;
+  a.extents = kExtHandles;
+  a.types = d_types;
+  a.n = n_blocks;
+  a.mode = kModeSstSeal;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_sst_verify_dev(const uint8_t* d_file,
+                                                               const uint64_t* d_handles,
+                                                               uint64_t n_blocks, uint8_t* d_ok,
+                                                               uint32_t* d_nbad, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_file || !d_handles || !d_ok) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_file;
+  a.handles = d_handles;
+  a.extents = kExtHandles;
+  a.n = n_blocks;
+  a.ok = d_ok;
+  a.nbad = d_nbad;
+  a.mode = kModeSstVerify;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes,
+                                                                    uint64_t seed, void* stream) {
+  if (nbytes == 0) return LSBM_OK;
+  if (!d_buf || (reinterpret_cast<uintptr_t>(d_buf) & 15))
+    return fail(LSBM_ERR_INVALID, "buffer must be 16-B aligned");
+  DeviceState* st = nullptr;
+  int rc = current_device(&st);
+  if (rc != LSBM_OK) return rc;
+  hipError_t e = launch_fill(static_cast<uint8_t*>(d_buf), nbytes, seed, st->num_cus * 8,
+                             static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LSBM_OK : fail_hip(e, "fill_splitmix64_kernel");
+}
+
+__attribute__((visibility("default"))) int lsbm_stream_read_dev(const void* d_buf, uint64_t nbytes,
+                                                                uint32_t* d_sink, void* stream) {
+  if (!d_buf || !d_sink || (reinterpret_cast<uintptr_t>(d_buf) & 15) || (nbytes & 15))
+    return fail(LSBM_ERR_INVALID, "buffer must be 16-B aligned, nbytes % 16 == 0");
+  DeviceState* st = nullptr;
+  int rc = current_device(&st);
+  if (rc != LSBM_OK) return rc;
+  hipError_t e = launch_stream_read(d_buf, nbytes, d_sink, st->num_cus * 8,
+                                    static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LSBM_OK : fail_hip(e, "stream_read_kernel");
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, const void* h_base,
+                                                                  const uint64_t* h_offsets,
+                                                                  uint64_t n_blocks,
+                                                                  const uint32_t* h_init,
+                                                                  uint32_t* h_out,
+                                                                  uint32_t flags) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!h_base || !h_offsets || !h_out) return fail(LSBM_ERR_INVALID, "null pointer");
+  if (flags & ~LSBM_CRC32C_MASKED) return fail(LSBM_ERR_INVALID, "unknown flags");
+  DeviceState* st = nullptr;
+  int rc = ensure_device(device, &st);
+  if (rc != LSBM_OK) return rc;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  Staging& stg = g_staging[device];
+  std::lock_guard<std::mutex> lock(stg.mu);
+  const uint8_t* src = static_cast<const uint8_t*>(h_base);
+  constexpr uint64_t kChunkBytes = 64ull << 20;
+  constexpr uint64_t kChunkBlocks = 1ull << 16;
+  const int nslots = 3;
+  int si = 0;
+  uint64_t next = 0;
+  rc = LSBM_OK;
+
+  auto drain = [&](Slot& s) -> int {
+    if (!s.busy) return LSBM_OK;
+    hipError_t ee = hipEventSynchronize(s.done);
+    s.busy = false;
+    if (ee != hipSuccess) return fail_hip(ee, "staged chunk");
+    memcpy(h_out + s.first, s.h_out, s.count * 4);
+    return LSBM_OK;
+  };
+
+  while (next < n_blocks && rc == LSBM_OK) {
+    // choose the chunk [next, last)
+    uint64_t bytes = 0, last = next;
+    while (last < n_blocks && last - next < kChunkBlocks) {
+      const uint64_t s0 = h_offsets[last], s1 = h_offsets[last + 1];
+      const uint64_t len = s1 > s0 ? s1 - s0 : 0;
+      if (last > next && bytes + len > kChunkBytes) break;
+      bytes += len;
+      last++;
+    }
+    Slot& s = stg.slot[si];
+    si = (si + 1) % nslots;
+    rc = drain(s);
+    if (rc != LSBM_OK) break;
+    e = reserve_slot(s, bytes + 16, last - next);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "staging buffers");
+      break;
+    }
+    // gather into pinned memory with rebased offsets (16-B aligned start)
+    uint64_t pos = 0;
+    for (uint64_t i = next; i < last; i++) {
+      const uint64_t s0 = h_offsets[i], s1 = h_offsets[i + 1];
+      const uint64_t len = s1 > s0 ? s1 - s0 : 0;
+      s.h_off[i - next] = pos;
+      memcpy(s.h_data + pos, src + s0, len);
+      pos += len;
+    }
+    s.h_off[last - next] = pos;
+    const uint64_t cnt = last - next;
+    if (h_init) memcpy(s.h_init, h_init + next, cnt * 4);
+    e = hipMemcpyAsync(s.d_data, s.h_data, pos, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess && h_init)
+      e = hipMemcpyAsync(s.d_init, s.h_init, cnt * 4, hipMemcpyHostToDevice, s.stream);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "H2D");
+      break;
+    }
+    RaggedArgs a = {};
+    a.base = s.d_data;
+    a.offsets = s.d_off;
+    a.n = cnt;
+    a.init = h_init ? s.d_init : nullptr;
+    a.out = s.d_out;
+    a.flags = flags;
+    a.mode = kModeOut;
+    a.dc = st->d_consts;
+    e = launch_ragged(a, grid_for(st, cnt), s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "staged launch");
+      break;
+    }
+    s.busy = true;
+    s.first = next;
+    s.count = cnt;
+    next = last;
+  }
+  for (int k = 0; k < nslots; k++) {
+    int r2 = drain(stg.slot[k]);
+    if (rc == LSBM_OK) rc = r2;
+  }
+  hipSetDevice(prev);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// crc32c_types.h -- layout shared by host (crc32c_engine.cc) and device
+// (crc32c_kernels.hip) code: geometry constants, the device table block and
+// the ragged-kernel argument block.  Plain C++, no HIP headers.
+#pragma once
+#include <stdint.h>
+
+namespace lsbm {
+
+constexpr int kRowBytes = 128;
+constexpr int kGroupLanes = 8;
+constexpr int kWaveLanes = 64;
+constexpr int kBlockThreads = 1024;
+constexpr int kWavesPerWg = kBlockThreads / kWaveLanes;
+constexpr uint32_t kLdsByteTabBytes = 131072;
+constexpr uint32_t kLdsNibBase = kLdsByteTabBytes;  // byte offset of nibble tables
+constexpr uint32_t kNibA4 = kLdsNibBase + 0 * 512;
+constexpr uint32_t kNibA16 = kLdsNibBase + 1 * 512;
+constexpr uint32_t kNibA32 = kLdsNibBase + 2 * 512;
+constexpr uint32_t kNibA64 = kLdsNibBase + 3 * 512;
+constexpr uint32_t kLdsBytes = kLdsNibBase + 4 * 512;
+constexpr uint32_t kLdsWords = kLdsBytes / 4;
+
+// Tables in device global memory, built once per device by the host (gf2.h).
+struct DevConsts {
+  uint32_t row_byte[4 * 256];    // byte tables of A^128 (main step)
+  uint32_t t0[256];              // A^1 byte table (1-byte extension)
+  uint32_t pow_nib[64][128];     // nibble tables of A^(2^k), k = 0..63
+  uint32_t neg_nib[128][128];    // nibble tables of A^-z, z = 0..127
+  uint32_t neg4_nib[128];        // nibble tables of A^-4
+};
+
+// How the ragged kernel finds block i's extent [s, e).
+enum ExtentKind : uint32_t {
+  kExtOffsets = 0,  // [offsets[i], offsets[i+1])
+  kExtHandles = 1,  // [h[2i], h[2i] + h[2i+1])  (BlockHandle {offset, size})
+  kExtFixed = 2,    // [i*stride, i*stride + len)
+};
+
+enum RaggedMode : uint32_t {
+  kModeOut = 0,        // out[i] = crc (masked if flags & 1)
+  kModeVerify = 1,     // ok[i] = (crc == expect[i]); mismatches added to *nbad
+  kModeSstSeal = 2,    // write trailer [type][Mask(crc(block || type))] after the block
+  kModeSstVerify = 3,  // ok[i] = stored trailer == Mask(crc(block || type))
+};
+
+struct RaggedArgs {
+  const uint8_t* base;      // extents are byte offsets from here
+  const uint64_t* offsets;  // kExtOffsets
+  const uint64_t* handles;  // kExtHandles
+  uint64_t stride, len;     // kExtFixed
+  uint64_t n;
+  const uint32_t* init;  // nullable: per-block init CRC (crc32c::Extend)
+  uint32_t* out;
+  const uint32_t* expect;
+  uint8_t* ok;
+  uint32_t* nbad;
+  const uint8_t* types;  // kModeSstSeal
+  uint8_t* file;         // kModeSstSeal: writable alias of base
+  uint32_t flags;
+  uint32_t mode;
+  uint32_t extents;
+  const DevConsts* dc;
+};
+
+}  // namespace lsbm

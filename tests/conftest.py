@@ -1,0 +1,124 @@
+"""Shared fixtures.  `-m gpu` tests need a HIP device; everything else runs on CPU.
+
+The oracle (oracle/liboracle_crc32c.so, a plain-C restatement of lsbm's
+util/crc32c.cc) is test infrastructure: it is loaded here only as the checker.
+"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+TESTS = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(TESTS)
+sys.path.insert(0, REPO)
+sys.path.insert(0, TESTS)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP (MI355X) device")
+
+
+class Oracle:
+    """ctypes view of oracle/liboracle_crc32c.so."""
+
+    def __init__(self, path):
+        lib = ctypes.CDLL(path)
+        u32, u64, vp, sz = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t
+        lib.oracle_extend.restype = u32
+        lib.oracle_extend.argtypes = [u32, vp, sz]
+        lib.oracle_mask.restype = u32
+        lib.oracle_mask.argtypes = [u32]
+        lib.oracle_unmask.restype = u32
+        lib.oracle_unmask.argtypes = [u32]
+        lib.oracle_batch_offsets.restype = None
+        lib.oracle_batch_offsets.argtypes = [vp, vp, u64, vp, vp, ctypes.c_int]
+        lib.oracle_batch_fixed.restype = None
+        lib.oracle_batch_fixed.argtypes = [vp, u64, u64, u64, vp, vp, ctypes.c_int]
+        lib.oracle_batch_fixed_mt.restype = ctypes.c_int
+        lib.oracle_batch_fixed_mt.argtypes = [vp, u64, u64, u64, vp, ctypes.c_int]
+        lib.oracle_fill_splitmix64.restype = None
+        lib.oracle_fill_splitmix64.argtypes = [vp, u64, u64, u64]
+        lib.oracle_tables.restype = None
+        lib.oracle_tables.argtypes = [vp]
+        self.lib = lib
+
+    def extend(self, init, data, align=0):
+        data = bytes(data)
+        buf = ctypes.create_string_buffer(len(data) + 64)
+        base = (ctypes.addressof(buf) + 15) & ~15
+        ctypes.memmove(base + align, data, len(data))
+        return self.lib.oracle_extend(init & 0xFFFFFFFF, base + align, len(data))
+
+    def value(self, data):
+        return self.extend(0, data)
+
+    def mask(self, c):
+        return self.lib.oracle_mask(c & 0xFFFFFFFF)
+
+    def unmask(self, c):
+        return self.lib.oracle_unmask(c & 0xFFFFFFFF)
+
+    def batch_offsets(self, data, offsets, init=None, masked=False):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        out = np.empty(n, dtype=np.uint32)
+        ini = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+        self.lib.oracle_batch_offsets(data.ctypes.data, offsets.ctypes.data, n,
+                                      None if ini is None else ini.ctypes.data,
+                                      out.ctypes.data, 1 if masked else 0)
+        return out
+
+    def batch_fixed(self, data, stride, length, n, init=None, masked=False):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        out = np.empty(n, dtype=np.uint32)
+        ini = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+        self.lib.oracle_batch_fixed(data.ctypes.data, stride, length, n,
+                                    None if ini is None else ini.ctypes.data,
+                                    out.ctypes.data, 1 if masked else 0)
+        return out
+
+    def fill_splitmix64(self, byte_off, nbytes, seed):
+        out = np.empty(nbytes, dtype=np.uint8)
+        self.lib.oracle_fill_splitmix64(out.ctypes.data, byte_off, nbytes, seed)
+        return out
+
+
+def _build(target_dir, artefact):
+    path = os.path.join(REPO, target_dir, artefact)
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", os.path.join(REPO, target_dir)], check=True,
+                       stdout=subprocess.DEVNULL)
+    return path
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return Oracle(_build("oracle", "liboracle_crc32c.so"))
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(TESTS, "golden", "crc32c_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def product_lib():
+    _build("lsbm_amd/csrc", "../liblsbm_crc32c.so")
+    from lsbm_amd import _lib
+    return _lib.lib()
+
+
+@pytest.fixture(scope="session")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from lsbm_amd import engine
+    engine.init(0)
+    return torch

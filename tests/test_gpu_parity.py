@@ -1,0 +1,252 @@
+"""GPU parity: every kernel result through the C ABI == the oracle, bit for bit.
+
+The oracle (oracle/crc32c_oracle.c) is pinned to lsbm's own util/crc32c.cc by
+tests/test_oracle.py.  Small/medium cases are checked block-for-block; the
+full-size benchmark configs are checked on sampled blocks plus
+size-independent properties (two independent kernels agree on every block;
+known golden blocks of each config buffer).
+"""
+import numpy as np
+import pytest
+
+from golden.splitmix import printable_bytes, stream_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(torch, arr, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if dtype is not None:
+        t = t.view(dtype)
+    return t.to("cuda")
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+# ---------------------------------------------------------------- fixed-stride
+@pytest.mark.parametrize("length,stride,n", [
+    (128, 128, 1), (128, 128, 9), (256, 256, 17), (512, 640, 33), (4096, 4096, 1),
+    (4096, 4096, 7), (4096, 4096, 1000), (4096, 8192, 129), (8192, 8192, 65),
+    (65536, 65536, 24), (384, 384, 100), (1152, 1280, 50), (640, 640, 41),
+])
+@pytest.mark.parametrize("use_init,masked", [(False, False), (True, False), (False, True)])
+def test_fixed_fast_path(torch_cuda, oracle, length, stride, n, use_init, masked):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    nbytes = (n - 1) * stride + length
+    data = stream_bytes(length * 131 + n + stride, 0, nbytes)
+    rng = np.random.default_rng(length + n)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if use_init else None
+    d = _dev(torch, data)
+    di = _dev(torch, init, torch.int32) if use_init else None
+    got = _u32(engine.crc32c_fixed(d, stride, length, n, init=di, masked=masked))
+    want = oracle.batch_fixed(data, stride, length, n, init, masked)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("length,stride,n,shift", [
+    (4118, 4118, 64, 0), (4117, 4123, 31, 0), (1, 1, 100, 0), (0, 16, 5, 0), (100, 100, 77, 0),
+    (4096, 4096, 20, 3), (4096, 4100, 20, 0), (70000, 70001, 5, 1), (3, 5, 1000, 0),
+])
+def test_fixed_general_geometry(torch_cuda, oracle, length, stride, n, shift):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    nbytes = (n - 1) * stride + length + shift
+    data = stream_bytes(777 + length, 0, nbytes)
+    d = _dev(torch, data)[shift:]  # misaligned base
+    got = _u32(engine.crc32c_fixed(d, stride, length, n))
+    want = oracle.batch_fixed(data[shift:], stride, length, n)
+    assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------- ragged
+def _ragged_case(seed, n, max_len, gap_max=0):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len + 1, size=n)
+    lens[rng.random(n) < 0.05] = 0
+    gaps = rng.integers(0, gap_max + 1, size=n) if gap_max else np.zeros(n, dtype=np.int64)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    pos = int(rng.integers(0, 16))
+    for i in range(n):
+        pos += int(gaps[i])
+        offs[i] = pos
+        pos += int(lens[i])
+    offs[n] = pos
+    # offsets array is [start_i] + end of last; with gaps the extents are
+    # [offs[i], offs[i]+lens[i]) -- express them as a dense extent list instead
+    starts = offs[:n]
+    ends = starts + lens
+    return starts, ends, pos
+
+
+@pytest.mark.parametrize("seed,n,max_len", [(1, 1, 10), (2, 100, 300), (3, 1000, 5000),
+                                            (4, 300, 70000), (5, 4096, 129), (6, 17, 4)])
+@pytest.mark.parametrize("use_init,masked", [(False, False), (True, True)])
+def test_ragged_dense(torch_cuda, oracle, seed, n, max_len, use_init, masked):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    starts, ends, total = _ragged_case(seed, n, max_len)
+    offs = np.concatenate([starts, ends[-1:]]).astype(np.int64)
+    data = stream_bytes(seed * 1000, 0, total + 64)
+    rng = np.random.default_rng(seed)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if use_init else None
+    got = _u32(engine.crc32c_batch(_dev(torch, data), _dev(torch, offs),
+                                   init=_dev(torch, init, torch.int32) if use_init else None,
+                                   masked=masked))
+    want = oracle.batch_offsets(data, offs.astype(np.uint64), init, masked)
+    assert np.array_equal(got, want)
+
+
+def test_ragged_unsorted_overlapping_extents(torch_cuda, oracle):
+    """offsets need not be monotone; extents may overlap or be empty (e < s -> empty)."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    data = stream_bytes(4242, 0, 200000)
+    rng = np.random.default_rng(9)
+    offs = rng.integers(0, 200000, size=5001).astype(np.int64)
+    got = _u32(engine.crc32c_batch(_dev(torch, data), _dev(torch, offs)))
+    want = np.empty(5000, dtype=np.uint32)
+    for i in range(5000):
+        s, e = int(offs[i]), int(offs[i + 1])
+        want[i] = oracle.value(data[s:max(s, e)].tobytes())
+    assert np.array_equal(got, want)
+
+
+def test_ragged_matches_fixed_on_same_blocks(torch_cuda):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n, L = 4096, 4096
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 123)
+    offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device="cuda")
+    a = engine.crc32c_fixed(d, L, L, n)
+    b = engine.crc32c_batch(d, offs)
+    assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------- verify
+def test_verify_detects_single_byte_flips(torch_cuda, oracle):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    starts, ends, total = _ragged_case(11, 2000, 6000)
+    offs = np.concatenate([starts, ends[-1:]]).astype(np.int64)
+    data = stream_bytes(11, 0, total + 16)
+    expect = oracle.batch_offsets(data, offs.astype(np.uint64), masked=True)
+    d = _dev(torch, data)
+    do = _dev(torch, offs)
+    ok, nbad = engine.crc32c_verify(d, do, _dev(torch, expect, torch.int32), masked=True)
+    assert int(nbad.item()) == 0 and bool(ok.all())
+    rng = np.random.default_rng(3)
+    bad = set()
+    for i in rng.choice(2000, size=50, replace=False):
+        if ends[i] > starts[i]:
+            pos = int(rng.integers(starts[i], ends[i]))
+            d[pos] ^= 1 << int(rng.integers(0, 8))
+            bad.add(int(i))
+    ok, nbad = engine.crc32c_verify(d, do, _dev(torch, expect, torch.int32), masked=True)
+    okh = ok.cpu().numpy()
+    assert int(nbad.item()) == len(bad)
+    assert set(np.nonzero(okh == 0)[0].tolist()) == bad
+
+
+# ---------------------------------------------------------------- SSTable trailers
+def test_sst_seal_matches_reference_trailers(torch_cuda, golden):
+    torch = torch_cuda
+    from lsbm_amd import table
+    blocks = golden["sst_blocks"]
+    handles, total = table.layout_blocks([b["len"] for b in blocks])
+    img = np.zeros(total, dtype=np.uint8)
+    for i, b in enumerate(blocks):
+        off = handles[2 * i]
+        img[off:off + b["len"]] = printable_bytes(b["seed"], b["len"])
+    d = _dev(torch, img)
+    dh = _dev(torch, handles.astype(np.int64))
+    types = _dev(torch, np.array([b["type"] for b in blocks], dtype=np.uint8))
+    table.seal_blocks(d, dh, types)
+    out = d.cpu().numpy()
+    for i, b in enumerate(blocks):
+        t0 = handles[2 * i] + b["len"]
+        assert out[t0:t0 + 5].tobytes().hex() == b["trailer_hex"], i
+    st, ok = table.verify_status(d, dh)
+    assert st.ok() and bool(ok.all())
+    # ReadBlock: a flipped payload byte or type byte -> Corruption
+    d[int(handles[2 * 5]) + 100] ^= 0x20
+    d[int(handles[2 * 9] + blocks[9]["len"])] ^= 0x01  # the type byte
+    st, ok = table.verify_status(d, dh)
+    assert st.IsCorruption() and st.ToString() == "Corruption: block checksum mismatch"
+    assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == {5, 9}
+
+
+def test_sst_random_layout_roundtrip(torch_cuda, oracle):
+    torch = torch_cuda
+    from lsbm_amd import table
+    rng = np.random.default_rng(21)
+    sizes = rng.integers(0, 9000, size=3000)
+    handles, total = table.layout_blocks(sizes)
+    img = stream_bytes(21, 0, total)
+    types = rng.integers(0, 2, size=3000).astype(np.uint8)
+    d = _dev(torch, img)
+    dh = _dev(torch, handles.astype(np.int64))
+    table.seal_blocks(d, dh, _dev(torch, types))
+    out = d.cpu().numpy()
+    for i in rng.choice(3000, size=200, replace=False):
+        off, n = int(handles[2 * i]), int(sizes[i])
+        crc = oracle.extend(oracle.value(out[off:off + n].tobytes()), bytes([types[i]]))
+        assert out[off + n] == types[i]
+        assert int.from_bytes(out[off + n + 1:off + n + 5].tobytes(), "little") == oracle.mask(crc)
+    ok, nbad = table.verify_blocks(d, dh)
+    assert int(nbad.item()) == 0
+
+
+# ---------------------------------------------------------------- host-staged
+def test_host_staged_batch(torch_cuda, oracle):
+    from lsbm_amd import engine
+    starts, ends, total = _ragged_case(31, 20000, 12000)
+    offs = np.concatenate([starts, ends[-1:]]).astype(np.uint64)
+    data = stream_bytes(31, 0, total)
+    init = np.random.default_rng(0).integers(0, 2**32, size=20000,
+                                              dtype=np.uint64).astype(np.uint32)
+    got = engine.crc32c_batch_host(data, offs, init=init, masked=True)
+    want = oracle.batch_offsets(data, offs, init, masked=True)
+    assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------- generator
+def test_fill_splitmix64_matches_numpy(torch_cuda):
+    torch = torch_cuda
+    from lsbm_amd import engine
+    for n, seed in [(1 << 20, 0x5EED0000), (1000003, 77)]:
+        d = torch.empty(n, dtype=torch.uint8, device="cuda")
+        engine.fill_splitmix64(d, seed)
+        assert np.array_equal(d.cpu().numpy(), stream_bytes(seed, 0, n))
+
+
+# ---------------------------------------------------------------- full-size configs
+def _config_fixed(torch, oracle, golden, name, seed, L, n, check_ragged_blocks):
+    from lsbm_amd import engine
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, seed)
+    crc = engine.crc32c_fixed(d, L, L, n)
+    got = _u32(crc)
+    for g in golden["config_blocks"]:
+        if g["config"] == name:
+            assert got[g["block"]] == g["value"], g
+    rng = np.random.default_rng(seed)
+    for b in rng.choice(n, size=256, replace=False):
+        assert got[b] == oracle.value(stream_bytes(seed, int(b) * L, L).tobytes()), b
+    # an independent kernel (ragged path, aligned frame, A^-z tail fix) agrees
+    m = min(n, check_ragged_blocks)
+    offs = torch.arange(0, (m + 1) * L, L, dtype=torch.int64, device="cuda")
+    other = engine.crc32c_batch(d, offs)
+    assert torch.equal(other, crc[:m])
+    del d
+
+
+def test_config2_full_1M_x_4KiB(torch_cuda, oracle, golden):
+    _config_fixed(torch_cuda, oracle, golden, "cfg2_4k", 0x5EED0000, 4096, 1 << 20, 1 << 20)
+
+
+def test_config3_full_1M_x_64KiB(torch_cuda, oracle, golden):
+    _config_fixed(torch_cuda, oracle, golden, "cfg3_64k", 0x5EED0001, 65536, 1 << 20, 1 << 16)
