@@ -106,8 +106,9 @@ int lsbm_crc32c_batch_host(int device, const void* h_base, const uint64_t* h_off
 /* ---- benchmark / diagnostic helpers (not on the checksum path) ---- */
 /* d_buf[k] = byte k of the splitmix64 stream `seed`. */
 int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream);
-/* Reads nbytes (16-B aligned, multiple of 16) once with 16-B loads and writes
- * one xor word per workgroup into d_sink[0..1023]: the stream-read ceiling. */
+/* Reads nbytes (16-B aligned, multiple of 16) once, with the CRC kernels' own
+ * access pattern (8 x 4 KiB blocks per wave as 128-B rows, 16-B non-temporal
+ * loads), into d_sink[0..1023]: the measured read ceiling for that pattern. */
 int lsbm_stream_read_dev(const void* d_buf, uint64_t nbytes, uint32_t* d_sink, void* stream);
 
 #ifdef __cplusplus

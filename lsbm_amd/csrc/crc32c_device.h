@@ -9,9 +9,12 @@
 //     consecutive words of a braid are exactly 128 B apart, so each braid step
 //     is  s = A^128(s ^ w)  -- the reference's slice-by-4 STEP4
 //     (util/crc32c.cc:295-302) with tables for A^128 instead of A^4;
+//   * the register kept per braid is the *pre-lookup* word c = s ^ w, so one
+//     step is c' = T0[c.b0] ^ T1[c.b1] ^ T2[c.b2] ^ T3[c.b3] ^ w_next: four
+//     v_perm (addresses), four ds_read_b32, two v_bitop3 (3-input xor);
 //   * after the last row the 32 braid registers of a block are merged with
-//     A^4 (in-lane) and A^16 / A^32 / A^64 (across the 8 lanes) into the raw
-//     CRC, using the identity crc(X||Y) = A^|Y|(crc(X)) ^ crc(Y).
+//     A^4 (in-lane, 3x), one lane-specific A^(116-16li) and a 3-step xor
+//     reduction across the 8 lanes, using crc(X||Y) = A^|Y|(crc(X)) ^ crc(Y).
 //
 // LDS image (one workgroup per CU, 1024 threads):
 //   [0, 128 KiB)   byte tables of A^128, replicated 32x so that lane l of every
@@ -19,8 +22,9 @@
 //                  random lookups.  Byte address of entry (table t, index b):
 //                      (t >> 1) << 16 | b << 8 | (t & 1) << 7 | (lane & 31) << 2
 //                  so one and-or builds the address from the state word.
-//   [128 KiB, +2K) nibble tables (16 entries each, hence conflict-free) of
-//                  A^4, A^16, A^32, A^64.
+//   0x20000        nibble tables of A^4 (16 entries each: conflict-free)
+//   0x20800        nibble tables of A^(116-16li), replicated per lane slot
+//                  (lane & 31) like the byte tables: conflict-free.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,26 +34,29 @@
 namespace lsbm {
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* lds, uint32_t byte_addr) {
+#ifdef LSBM_ABL_NO_LDS  // diagnostic builds only (tools/ablate.sh): a VALU op instead
+  return byte_addr * 0x9e3779b1u;
+#else
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+#endif
 }
 
-// One braid step over the state word c = s ^ w: A^128(c) via the replicated
-// byte tables (L[t] = the lane's constant part of the table-t address).
-__device__ __forceinline__ uint32_t row_step(const uint32_t* lds, uint32_t c, uint32_t L0,
-                                             uint32_t L1, uint32_t L2, uint32_t L3) {
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32
+}
+
+// One braid step: A^128(c) ^ w via the replicated byte tables (L[t] = the
+// lane's constant part of the table-t address), i.e. the reference's STEP4
+// (util/crc32c.cc:295-302) for a 128-byte stride, with the next word folded in.
+__device__ __forceinline__ uint32_t row_step(const uint32_t* lds, uint32_t c, uint32_t w,
+                                             uint32_t L0, uint32_t L1, uint32_t L2,
+                                             uint32_t L3) {
   const uint32_t a0 = __builtin_amdgcn_perm(c, L0, 0x0c020400u);  // byte0 of c -> bits 8..15
   const uint32_t a1 = __builtin_amdgcn_perm(c, L1, 0x0c020500u);  // byte1
   const uint32_t a2 = __builtin_amdgcn_perm(c, L2, 0x0c020600u);  // byte2
   const uint32_t a3 = __builtin_amdgcn_perm(c, L3, 0x0c020700u);  // byte3
-  return lds_load(lds, a0) ^ lds_load(lds, a1) ^ lds_load(lds, a2) ^ lds_load(lds, a3);
-}
-
-// M(v) for a matrix given as nibble tables in LDS at byte offset `tab`.
-__device__ __forceinline__ uint32_t nib_lds(const uint32_t* lds, uint32_t tab, uint32_t v) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) r ^= lds_load(lds, tab + q * 64 + ((v >> (4 * q)) & 15u) * 4);
-  return r;
+  return xor3(xor3(lds_load(lds, a0), lds_load(lds, a1), lds_load(lds, a2)), lds_load(lds, a3),
+              w);
 }
 
 // M(v) for a matrix given as nibble tables in global memory (cached, rare use).
@@ -76,40 +83,66 @@ __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {  // util/crc32c.h:3
   return (r >> 17) | (r << 15);
 }
 
-// Fill the LDS image from DevConsts (whole workgroup, ends with a barrier).
-__device__ __forceinline__ void load_lds_tables(uint32_t* lds, const DevConsts* __restrict__ dc) {
-  for (uint32_t w = threadIdx.x; w < kLdsByteTabBytes / 4; w += blockDim.x) {
-    const uint32_t a = w << 2;
-    const uint32_t t = ((a >> 16) << 1) | ((a >> 7) & 1u);
-    const uint32_t b = (a >> 8) & 255u;
-    lds[w] = dc->row_byte[t * 256 + b];
+// A^4(v) from the uniform LDS nibble tables at kNibA4.
+__device__ __forceinline__ uint32_t adv4_lds(const uint32_t* lds, uint32_t v) {
+  uint32_t t[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t f = q == 0 ? (v << 2) : (v >> (4 * q - 2));  // nibble q -> bits 2..5
+    t[q] = lds_load(lds, ((f & 0x3cu) | kNibA4) + q * 64);
   }
-  for (uint32_t w = threadIdx.x; w < 4 * 128; w += blockDim.x) {
-    const uint32_t tab = w >> 7, e = w & 127u;
-    const int k = tab == 0 ? 2 : (tab == 1 ? 4 : (tab == 2 ? 5 : 6));  // A^4, ^16, ^32, ^64
-    lds[kLdsNibBase / 4 + w] = dc->pow_nib[k][e];
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// A^(116-16li)(v) from the lane-replicated LDS tables at kNibFin.
+// lane_fin = kNibFin | (lane & 31) << 2.
+__device__ __forceinline__ uint32_t fin_lds(const uint32_t* lds, uint32_t v, uint32_t lane_fin) {
+  uint32_t t[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t f = q == 0 ? (v << 7) : (q == 1 ? (v << 3) : (v >> (4 * q - 7)));
+    t[q] = lds_load(lds, ((f & 0x780u) | lane_fin) + q * 2048);  // nibble q -> bits 7..10
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// Copy the prebuilt LDS image (DevConsts::lds_image) into LDS: every thread
+// issues all of its 16-B loads before its first LDS write (one round trip).
+__device__ __forceinline__ void load_lds_tables(uint32_t* lds, const DevConsts* __restrict__ dc) {
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  constexpr uint32_t kChunks = kLdsBytes / 16;
+  constexpr uint32_t kPer = (kChunks + kBlockThreads - 1) / kBlockThreads;
+  const v4* __restrict__ src = reinterpret_cast<const v4*>(dc->lds_image);
+  v4* dst = reinterpret_cast<v4*>(lds);
+  v4 t[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) {
+    const uint32_t i = threadIdx.x + k * kBlockThreads;
+    if (i < kChunks) t[k] = src[i];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) {
+    const uint32_t i = threadIdx.x + k * kBlockThreads;
+    if (i < kChunks) dst[i] = t[k];
   }
   __syncthreads();
 }
 
-// Merge a group's 32 braid registers into the raw CRC of the rows they cover,
-// positioned at the end of the last row.  li = lane within the 8-lane group.
-// Valid on lane li == 7 only.
-__device__ __forceinline__ uint32_t merge_braids(const uint32_t* lds, uint32_t s0, uint32_t s1,
-                                                 uint32_t s2, uint32_t s3, uint32_t li) {
+// Merge a group's 32 braid registers (c_m = pre-lookup word of braid m after
+// the last row) into the raw CRC of the rows they cover, positioned at the
+// end of the last row.  Every lane of the group gets the result.
+__device__ __forceinline__ uint32_t merge_braids(const uint32_t* lds, uint32_t c0, uint32_t c1,
+                                                 uint32_t c2, uint32_t c3, uint32_t lane_fin) {
   // in-lane: words at 16li + 0, 4, 8, 12 -> one register at 16li + 12
-  uint32_t u = nib_lds(lds, kNibA4, s0) ^ s1;
-  u = nib_lds(lds, kNibA4, u) ^ s2;
-  u = nib_lds(lds, kNibA4, u) ^ s3;
-  // across lanes: pairs 16 B apart, then 32 B, then 64 B
-  uint32_t t = __shfl_up(nib_lds(lds, kNibA16, u), 1, kGroupLanes);
-  if (li & 1u) u ^= t;
-  t = __shfl_up(nib_lds(lds, kNibA32, u), 2, kGroupLanes);
-  if ((li & 3u) == 3u) u ^= t;
-  t = __shfl_up(nib_lds(lds, kNibA64, u), 4, kGroupLanes);
-  if (li == 7u) u ^= t;
-  // lane 7 now holds the state positioned at the last word (row offset 124)
-  return nib_lds(lds, kNibA4, u);
+  uint32_t u = adv4_lds(lds, c0) ^ c1;
+  u = adv4_lds(lds, u) ^ c2;
+  u = adv4_lds(lds, u) ^ c3;
+  // to the end of the row: A^(128 - (16li + 16)) then A^4 = A^(116 - 16li)
+  u = fin_lds(lds, u, lane_fin);
+  u ^= __shfl_xor(u, 1, kGroupLanes);
+  u ^= __shfl_xor(u, 2, kGroupLanes);
+  u ^= __shfl_xor(u, 4, kGroupLanes);
+  return u;
 }
 
 }  // namespace lsbm

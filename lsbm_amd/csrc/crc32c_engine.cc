@@ -66,6 +66,20 @@ void build_consts(DevConsts* c) {
   }
   for (int z = 0; z < 128; z++) gf2::nibble_tables(gf2::byte_pow(-z), c->neg_nib[z]);
   gf2::nibble_tables(gf2::byte_pow(-4), c->neg4_nib);
+  for (int li = 0; li < 8; li++) gf2::nibble_tables(gf2::byte_pow(116 - 16 * li), c->fin_nib[li]);
+  // LDS image (layout: crc32c_device.h header comment)
+  memset(c->lds_image, 0, sizeof(c->lds_image));
+  for (uint32_t w = 0; w < kLdsByteTabBytes / 4; w++) {
+    const uint32_t a = w << 2;
+    const uint32_t t = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t b = (a >> 8) & 255u;
+    c->lds_image[w] = c->row_byte[t * 256 + b];
+  }
+  for (uint32_t w = 0; w < 128; w++) c->lds_image[kNibA4 / 4 + w] = c->pow_nib[2][w];
+  for (uint32_t w = 0; w < 8 * 16 * 32; w++) {
+    const uint32_t q = w >> 9, nib = (w >> 5) & 15u, slot = w & 31u;
+    c->lds_image[kNibFin / 4 + w] = c->fin_nib[slot & 7u][q * 16 + nib];
+  }
 }
 
 void init_device(int dev, DeviceState* st) {
@@ -237,7 +251,8 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
   if (rc != LSBM_OK) return rc;
   const uintptr_t b = reinterpret_cast<uintptr_t>(d_base);
   const bool fast = (b % 16 == 0) && (stride % 16 == 0) && len >= kRowBytes &&
-                    (len % kRowBytes == 0) && (len / kRowBytes) <= 0xffffffffull;
+                    (len % kRowBytes == 0) && stride >= len && stride <= (1ull << 28) &&
+                    n_blocks < (1ull << 34);
   if (fast) {
     const gf2::Mat an = gf2::byte_pow((int64_t)len);
     const uint32_t k_value = gf2::apply(an, 0xffffffffu) ^ 0xffffffffu;
@@ -351,7 +366,7 @@ __attribute__((visibility("default"))) int lsbm_stream_read_dev(const void* d_bu
   DeviceState* st = nullptr;
   int rc = current_device(&st);
   if (rc != LSBM_OK) return rc;
-  hipError_t e = launch_stream_read(d_buf, nbytes, d_sink, st->num_cus * 8,
+  hipError_t e = launch_stream_read(d_buf, nbytes, d_sink, st->num_cus,
                                     static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "stream_read_kernel");
 }

@@ -22,47 +22,51 @@ __shared__ uint32_t g_lds[kLdsWords];
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr uint32_t kPF = 4;  // rows per load bank
+#ifdef LSBM_DIAG_STAMPS  // diagnostic builds only (tools/ablate.sh): per-wave timeline
+__device__ uint64_t g_stamps[4][65536];  // start, first-data, end, xcc id
+extern "C" __attribute__((visibility("default"))) int lsbm_diag_stamps(uint64_t* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(uint64_t) * 4 * 65536) == hipSuccess ? 0 : -1;
+}
+#define DIAG_STAMP(k) do { if (lane == 0) g_stamps[k][wave & 65535] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define DIAG_STAMP(k) do { } while (0)
+#endif
+
+#ifndef LSBM_PF
+#define LSBM_PF 4
+#endif
+constexpr uint32_t kPF = LSBM_PF;  // rows per load bank
+
+constexpr int kAuxNT = 2;     // buffer-load cache policy: non-temporal (read-once stream)
 
 // Issue the loads of rows [r0, r0 + kPF) of this lane's slice into bank X.
-// Always kPF loads (rows past the end re-read the last row, a cache hit) so
-// that the compiler can count outstanding loads exactly; `rows` is uniform.
-#define LOAD_BANK(X, r0)                                                        \
-  do {                                                                          \
-    _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPF; k_++) {                   \
-      const uint32_t rr_ = (r0) + k_ < rows ? (r0) + k_ : rows - 1;             \
-      X[k_] = __builtin_nontemporal_load(p + rr_ * 8);                          \
-    }                                                                           \
+// Rows past the end re-read the last row (clamped, a cache hit), so the
+// number of loads in flight is static and the compiler's vmcnt waits exact.
+#define LOAD_BANK(X, r0)                                                          \
+  do {                                                                            \
+    _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPF; k_++) {                     \
+      const uint32_t rr_ = (r0) + k_ < rows ? (r0) + k_ : rows - 1;               \
+      X[k_] = __builtin_bit_cast(                                                 \
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, loff + rr_ * kRowBytes, 0, \
+                                                       kAuxNT));                  \
+    }                                                                             \
   } while (0)
 
-#define STEP_ROW(W)                                          \
-  do {                                                       \
-    s0 = row_step(g_lds, s0 ^ (W).x, L0, L1, L2, L3);        \
-    s1 = row_step(g_lds, s1 ^ (W).y, L0, L1, L2, L3);        \
-    s2 = row_step(g_lds, s2 ^ (W).z, L0, L1, L2, L3);        \
-    s3 = row_step(g_lds, s3 ^ (W).w, L0, L1, L2, L3);        \
-  } while (0)
-
-// All kPF rows of the bank are followed by more rows: advance by 128 B each.
-#define ABSORB_FULL(X)                                              \
-  do {                                                              \
-    _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPF; k_++) STEP_ROW(X[k_]); \
-  } while (0)
-
-// The bank holds the block's last row: rows before it advance, the last row
-// is only xor-ed in (its registers are merged by merge_braids).
-#define ABSORB_TAIL(X, r0)                                    \
+// c_m = A^128(c_m) ^ w_m for the four braids of one 16-B row slice.
+#define STEP_ROW(W)                                           \
   do {                                                        \
-    _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPF; k_++) { \
-      if ((r0) + k_ + 1 < rows) {                             \
-        STEP_ROW(X[k_]);                                      \
-      } else if ((r0) + k_ + 1 == rows) {                     \
-        s0 ^= X[k_].x;                                        \
-        s1 ^= X[k_].y;                                        \
-        s2 ^= X[k_].z;                                        \
-        s3 ^= X[k_].w;                                        \
-      }                                                       \
-    }                                                         \
+    c0 = row_step(g_lds, c0, (W).x, L0, L1, L2, L3);          \
+    c1 = row_step(g_lds, c1, (W).y, L0, L1, L2, L3);          \
+    c2 = row_step(g_lds, c2, (W).z, L0, L1, L2, L3);          \
+    c3 = row_step(g_lds, c3, (W).w, L0, L1, L2, L3);          \
+  } while (0)
+
+// Absorb the rows of bank X that exist (rows r0 .. r0+kPF-1).
+#define ABSORB(X, r0)                                                       \
+  do {                                                                      \
+    _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPF; k_++) {               \
+      if ((r0) + k_ < rows) STEP_ROW(X[k_]);                                \
+    }                                                                       \
   } while (0)
 
 // ---------------------------------------------------------------------------
@@ -76,56 +80,76 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     uint32_t k_value /* A^len(~0) ^ ~0: the init term of crc32c::Value */,
     const DevConsts* __restrict__ dc) {
   const uint32_t rows = kRows ? kRows : rows_arg;  // kRows != 0: fully unrolled
-  load_lds_tables(g_lds, dc);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
   const uint32_t lb = (lane & 31u) << 2;
   const uint32_t L0 = lb, L1 = lb | 0x80u, L2 = lb | 0x10000u, L3 = lb | 0x10080u;
-  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg + (threadIdx.x >> 6);
+  const uint32_t lane_fin = kNibFin | lb;
+  const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg + wave_in_wg;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
   const uint64_t ngroups = (n_blocks + 7) / 8;
 
-  for (uint64_t grp = wave; grp < ngroups; grp += nwaves) {
+  // The first group's first two banks are requested from HBM before the LDS
+  // tables are filled, so the table fill hides under the first HBM latency.
+  u32x4 a[kPF], b[kPF];
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t loff;
+  auto set_group = [&](uint64_t grp) {
+    const uint64_t blk = grp * 8 + g;
+    // wave-uniform descriptor over the group's 8 blocks; per-lane 32-bit
+    // offset (host guarantees 8 * stride < 2^32).  Lanes past the end re-read
+    // block 0 of the group and discard the result.
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + grp * 8 * stride),
+                                             (short)0, (int)0x7fffffff, 0x00020000);
+    loff = (blk < n_blocks ? g : 0u) * (uint32_t)stride + 16u * li;
+  };
+  // Static interleave: wave w takes groups w, w + nwaves, ...  At any moment
+  // the GPU streams one contiguous ~128 MiB window of the batch.  (A dynamic
+  // per-XCC work queue evened out per-wave finish times but was 5% slower
+  // end to end: DESIGN.md section 4.)
+  uint64_t grp = wave;
+  DIAG_STAMP(0);
+  if (grp < ngroups) {
+    set_group(grp);
+    LOAD_BANK(a, 0);
+    if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
+  }
+  load_lds_tables(g_lds, dc);
+  DIAG_STAMP(1);
+
+  bool first = true;
+  for (; grp < ngroups; grp += nwaves) {
     const uint64_t blk = grp * 8 + g;
     const bool valid = blk < n_blocks;
-    const u32x4* __restrict__ p =
-        reinterpret_cast<const u32x4*>(base + (valid ? blk : 0) * stride) + li;
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-
-    // Two banks of kPF rows each: while bank A is absorbed, bank B's loads
-    // are in flight (and vice versa), so every lane keeps kPF..2*kPF rows of
-    // 16 B outstanding without the compiler rotating registers.
-    u32x4 a[kPF], b[kPF];
-    LOAD_BANK(a, 0);
-    uint32_t r = 0;
-    // steady state: both banks hold rows that are followed by more rows
-    while (r + 3 * kPF <= rows) {
-      LOAD_BANK(b, r + kPF);
-      ABSORB_FULL(a);
-      LOAD_BANK(a, r + 2 * kPF);
-      ABSORB_FULL(b);
-      r += 2 * kPF;
+    // Two banks of kPF rows: while one bank is absorbed the other's loads
+    // are in flight.  Row 0 initialises the braids (c = w); every later row
+    // is c = A^128(c) ^ w.
+    if (!first) {
+      set_group(grp);
+      LOAD_BANK(a, 0);
+      if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
     }
-    // the last (up to 3) banks
-    while (true) {
-      if (r + kPF < rows) {
-        LOAD_BANK(b, r + kPF);
-        ABSORB_FULL(a);
-      } else {
-        ABSORB_TAIL(a, r);
-        break;
-      }
+    first = false;
+    uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
+#pragma unroll
+    for (uint32_t k = 1; k < kPF; k++)
+      if (k < rows) STEP_ROW(a[k]);
+    uint32_t r = kPF;
+    while (r < rows) {
+      if (kRows == 0 || r + kPF < rows) LOAD_BANK(a, r + kPF);
+      ABSORB(b, r);
       r += kPF;
-      if (r + kPF < rows) {
-        LOAD_BANK(a, r + kPF);
-        ABSORB_FULL(b);
-      } else {
-        ABSORB_TAIL(b, r);
-        break;
-      }
+      if (r >= rows) break;
+      if (kRows == 0 || r + kPF < rows) LOAD_BANK(b, r + kPF);
+      ABSORB(a, r);
       r += kPF;
     }
-    const uint32_t raw = merge_braids(g_lds, s0, s1, s2, s3, li);
+#ifdef LSBM_ABL_NO_MERGE  // diagnostic builds only (tools/ablate.sh)
+    const uint32_t raw = c0 ^ c1 ^ c2 ^ c3;
+#else
+    const uint32_t raw = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+#endif
     if (li == 7u && valid) {
       uint32_t crc;
       if (kHasInit)
@@ -136,8 +160,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
       out[blk] = (flags & 1u) ? mask_crc(crc) : crc;
     }
   }
+  DIAG_STAMP(2);
+#ifdef LSBM_DIAG_STAMPS
+  if (lane == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    g_stamps[3][wave & 65535] = xcc;
+  }
+#endif
 }
-
 // ---------------------------------------------------------------------------
 // Ragged kernel.  Same row/braid machinery, but rows are 128-B aligned in the
 // absolute address space, so every load is an aligned 16-B load whatever the
@@ -170,6 +201,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_ragged_kernel(RaggedArgs
   const uint32_t g = lane >> 3, li = lane & 7u;
   const uint32_t lb = (lane & 31u) << 2;
   const uint32_t L0 = lb, L1 = lb | 0x80u, L2 = lb | 0x10000u, L3 = lb | 0x10080u;
+  const uint32_t lane_fin = kNibFin | lb;
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
   const uint64_t ngroups = (args.n + 7) / 8;
@@ -200,7 +232,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_ragged_kernel(RaggedArgs
     const uint64_t rows = row_end > row0 ? row_end - row0 : 1;
     const uint32_t z = (uint32_t)((row0 + rows) * kRowBytes - e);
 
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // A^128(0) = 0: row 0 needs no special case
     for (uint64_t r = 0; r < rows; r++) {
       const uint64_t a = (row0 + r) * kRowBytes + 16u * li;
       u32x4 w = {0u, 0u, 0u, 0u};
@@ -213,19 +245,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_ragged_kernel(RaggedArgs
           w.w = frame_word(w.w, a + 12, s, e, u);
         }
       }
-      if (r + 1 < rows) {
-        s0 = row_step(g_lds, s0 ^ w.x, L0, L1, L2, L3);
-        s1 = row_step(g_lds, s1 ^ w.y, L0, L1, L2, L3);
-        s2 = row_step(g_lds, s2 ^ w.z, L0, L1, L2, L3);
-        s3 = row_step(g_lds, s3 ^ w.w, L0, L1, L2, L3);
-      } else {
-        s0 ^= w.x;
-        s1 ^= w.y;
-        s2 ^= w.z;
-        s3 ^= w.w;
-      }
+      STEP_ROW(w);
     }
-    const uint32_t padded = merge_braids(g_lds, s0, s1, s2, s3, li);
+    const uint32_t padded = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
     if (li == 7u && valid) {
       uint32_t l = nib_glb(dc->neg_nib[z], padded);  // register after the block
       if (args.mode == kModeSstSeal) {
@@ -292,23 +314,40 @@ __global__ void fill_splitmix64_kernel(uint8_t* __restrict__ buf, uint64_t nbyte
   }
 }
 
-__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
-                                                          uint32_t* __restrict__ sink) {
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+// Read ceiling for the CRC kernels' own access pattern: 1024-thread
+// workgroups, each wave reads 8 blocks of 4 KiB as 128-B rows (one 16-B
+// non-temporal load per lane per row), waves interleaved over 32 KiB groups;
+// a grid-stride loop covers any remainder.  Bytes are xor-folded so the
+// loads stay live.
+__global__ __launch_bounds__(kBlockThreads) void stream_read_kernel(const uint8_t* __restrict__ base,
+                                                                    uint64_t nbytes,
+                                                                    uint32_t* __restrict__ sink) {
+  const uint32_t lane = threadIdx.x & 63u, g = lane >> 3, li = lane & 7u;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
+  const uint64_t ngroups = nbytes / 32768;
   uint32_t acc = 0;
-  uint64_t i = tid;
-  for (; i + 3 * nthreads < n16; i += 4 * nthreads) {
-    const u32x4 a = __builtin_nontemporal_load(p + i);
-    const u32x4 b = __builtin_nontemporal_load(p + i + nthreads);
-    const u32x4 c = __builtin_nontemporal_load(p + i + 2 * nthreads);
-    const u32x4 d = __builtin_nontemporal_load(p + i + 3 * nthreads);
-    acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^
-           d.z ^ d.w;
+  for (uint64_t grp = wave; grp < ngroups; grp += nwaves) {
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(base + grp * 32768), (short)0, 32768, 0x00020000);
+    const uint32_t loff = g * 4096u + 16u * li;
+#pragma unroll
+    for (uint32_t r0 = 0; r0 < 32; r0 += 4) {
+      u32x4 v[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rsrc, loff + (r0 + k) * kRowBytes, 0, kAuxNT));
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) acc ^= xor3(v[k].x, v[k].y, v[k].z) ^ v[k].w;
+    }
   }
-  for (; i < n16; i += nthreads) {
-    const u32x4 a = p[i];
-    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  const uint64_t tail0 = ngroups * 32768;
+  for (uint64_t i = tail0 + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i + 16 <= nbytes;
+       i += (uint64_t)gridDim.x * blockDim.x * 16) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(base + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
   if (acc == 0x9e3779b9u) sink[blockIdx.x & 1023u] = acc;  // keeps the loads live
 }
@@ -320,11 +359,14 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
 #define LSBM_LAUNCH_FIXED(HI, R)                                                        \
   hipLaunchKernelGGL((crc32c_fixed_kernel<HI, R>), dim3(grid), dim3(kBlockThreads), 0, stream, \
                      base, stride, rows, n_blocks, init, out, flags, k_value, dc)
+  // compile-time row counts for the SSTable-sized configs: 4 KiB and 64 KiB
   if (init) {
     if (rows == 32) LSBM_LAUNCH_FIXED(true, 32);
+    else if (rows == 512) LSBM_LAUNCH_FIXED(true, 512);
     else LSBM_LAUNCH_FIXED(true, 0);
   } else {
-    if (rows == 32) LSBM_LAUNCH_FIXED(false, 32);  // 4 KiB blocks: the headline config
+    if (rows == 32) LSBM_LAUNCH_FIXED(false, 32);
+    else if (rows == 512) LSBM_LAUNCH_FIXED(false, 512);
     else LSBM_LAUNCH_FIXED(false, 0);
   }
 #undef LSBM_LAUNCH_FIXED
@@ -343,8 +385,8 @@ hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, int grid, h
 
 hipError_t launch_stream_read(const void* buf, uint64_t nbytes, uint32_t* sink, int grid,
                               hipStream_t stream) {
-  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(256), 0, stream,
-                     reinterpret_cast<const u32x4*>(buf), nbytes / 16, sink);
+  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(kBlockThreads), 0, stream,
+                     reinterpret_cast<const uint8_t*>(buf), nbytes, sink);
   return hipGetLastError();
 }
 

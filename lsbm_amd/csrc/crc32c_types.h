@@ -12,12 +12,12 @@ constexpr int kWaveLanes = 64;
 constexpr int kBlockThreads = 1024;
 constexpr int kWavesPerWg = kBlockThreads / kWaveLanes;
 constexpr uint32_t kLdsByteTabBytes = 131072;
-constexpr uint32_t kLdsNibBase = kLdsByteTabBytes;  // byte offset of nibble tables
-constexpr uint32_t kNibA4 = kLdsNibBase + 0 * 512;
-constexpr uint32_t kNibA16 = kLdsNibBase + 1 * 512;
-constexpr uint32_t kNibA32 = kLdsNibBase + 2 * 512;
-constexpr uint32_t kNibA64 = kLdsNibBase + 3 * 512;
-constexpr uint32_t kLdsBytes = kLdsNibBase + 4 * 512;
+// Nibble tables (byte offsets into LDS).  Bases are chosen so that an
+// and-or can merge the nibble field with the base (disjoint bits).
+constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
+constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
+                                         // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
+constexpr uint32_t kLdsBytes = kNibFin + 8 * 16 * 32 * 4;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
 // Tables in device global memory, built once per device by the host (gf2.h).
@@ -27,6 +27,10 @@ struct DevConsts {
   uint32_t pow_nib[64][128];     // nibble tables of A^(2^k), k = 0..63
   uint32_t neg_nib[128][128];    // nibble tables of A^-z, z = 0..127
   uint32_t neg4_nib[128];        // nibble tables of A^-4
+  uint32_t fin_nib[8][128];      // nibble tables of A^(116 - 16 li), li = 0..7 (merge)
+  // The kernels' LDS image, prebuilt by the host so that each workgroup
+  // fills its LDS with ~9 coalesced 16-B loads per thread.
+  alignas(16) uint32_t lds_image[kLdsWords];
 };
 
 // How the ragged kernel finds block i's extent [s, e).
