@@ -17,8 +17,8 @@ ranks.  Rank 0 prints ONE JSON line.
 
 Extra fields: roofline (achieved algorithmic GB/s of the dominant kernel vs the
 8 TB/s HBM peak), cpu_baseline (the reference CPU CRC on the host cores, rank 0
-at N=1 only, bounded sample), stream_read (a plain 16-B-per-lane read of the
-same buffer: the measured read ceiling).
+at N=1 only, bounded sample), stream_read (the same buffer read with the CRC
+kernel's own access pattern and no CRC work: the measured read ceiling).
 """
 import argparse
 import ctypes
@@ -49,6 +49,37 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="aggregate CPU-seconds for the cpu_baseline sample")
     return p.parse_args()
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous shard [lo, hi) of n_total independent blocks for `rank`.
+    Blocks never cross ranks: the CRC of a block needs only its own bytes."""
+    per = (n_total + world - 1) // world
+    lo = min(n_total, rank * per)
+    return lo, min(n_total, lo + per)
+
+
+def timed_steps(step, steps, warmup, sync, barrier, max_reduce, mark_start=None, mark_end=None):
+    """The driver's timing contract: `warmup` untimed steps, barrier +
+    synchronize, `steps` timed steps, barrier + synchronize.  Returns the MAX
+    over ranks of this rank's wall seconds for the timed region.  mark_start /
+    mark_end bracket exactly the timed launches (device events)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    if mark_start:
+        mark_start()
+    for _ in range(steps):
+        step()
+    if mark_end:
+        mark_end()
+    sync()
+    barrier()
+    sync()
+    return max_reduce(time.perf_counter() - t0)
 
 
 def load_traffic(workload):
@@ -139,30 +170,21 @@ def main():
     def step():
         engine.crc32c_fixed(data, BLOCK, BLOCK, n, out=out, stream=stream)
 
-    for _ in range(args.warmup):
-        step()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def barrier():
-        torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
 
-    barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1)  # K launches on the launch stream
-    t_local = max(wall, kern_ms / 1e3)
-    t = torch.tensor([t_local], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
+    def max_reduce(x):
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_max = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, barrier, max_reduce,
+                        mark_start=lambda: ev0.record(stream), mark_end=lambda: ev1.record(stream))
+    kern_ms = ev0.elapsed_time(ev1)  # the K launches, HIP events on the launch stream
 
     # stream-read ceiling on the same buffer (same stream, same events)
     sink = torch.zeros(1024, dtype=torch.int32, device="cuda")

@@ -1,0 +1,71 @@
+// include/lsbm/table_checksum.h -- C++ host API for lsbm's table/ layer:
+// batched SSTable block-trailer seal and verify over a host file image.
+//
+// Mirrors, for a whole batch of blocks, what the reference does per block:
+//   TableBuilder::WriteRawBlock (table/table_builder.cc:237-255)
+//       trailer = [type][EncodeFixed32(Mask(Extend(Value(block), &type, 1)))]
+//   ReadBlock with ReadOptions::verify_checksums (table/format.cc:95-103)
+//       Unmask(DecodeFixed32(data + n + 1)) == Value(data, n + 1)
+//       else Status::Corruption("block checksum mismatch")
+// Sits on top of the C ABI (include/lsbm_crc32c.h); all CRC work runs on the
+// GPU.  No HIP types in this header.
+#ifndef LSBM_TABLE_CHECKSUM_H_
+#define LSBM_TABLE_CHECKSUM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace lsbm {
+
+// table/format.h:22-50 (offset and size of a block inside a table file).
+struct BlockHandle {
+  uint64_t offset;
+  uint64_t size;
+};
+
+// include/leveldb/options.h:24-29
+enum CompressionType : uint8_t { kNoCompression = 0x0, kSnappyCompression = 0x1 };
+
+// table/format.h:84
+static const size_t kBlockTrailerSize = 5;
+
+// The subset of leveldb::Status (include/leveldb/status.h) this layer returns.
+class Status {
+ public:
+  Status() : code_(kOk) {}
+  static Status OK() { return Status(); }
+  static Status Corruption(const std::string& msg) { return Status(kCorruption, msg); }
+  static Status InvalidArgument(const std::string& msg) { return Status(kInvalidArgument, msg); }
+  static Status IOError(const std::string& msg) { return Status(kIOError, msg); }
+  bool ok() const { return code_ == kOk; }
+  bool IsCorruption() const { return code_ == kCorruption; }
+  std::string ToString() const;
+
+ private:
+  enum Code { kOk = 0, kCorruption = 2, kInvalidArgument = 4, kIOError = 5 };
+  Status(Code c, const std::string& m) : code_(c), msg_(m) {}
+  Code code_;
+  std::string msg_;
+};
+
+// Lay n blocks of the given sizes back to back, each followed by its 5-byte
+// trailer (offset += size + kBlockTrailerSize, table/table_builder.cc:251).
+// Returns the handles; *file_size receives the total image size.
+std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64_t* file_size);
+
+// Batched WriteRawBlock: for every handle, writes the trailer at
+// file[offset + size, offset + size + 5) with type = types[i].
+Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
+                  const uint8_t* types, size_t n);
+
+// Batched ReadBlock verify.  ok (optional) receives one flag per block.
+// Returns Corruption("block checksum mismatch") if any block fails.
+Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
+                    size_t n, std::vector<uint8_t>* ok);
+
+}  // namespace lsbm
+
+#endif  // LSBM_TABLE_CHECKSUM_H_

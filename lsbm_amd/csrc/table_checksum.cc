@@ -1,0 +1,121 @@
+// table_checksum.cc -- include/lsbm/table_checksum.h on top of the C ABI.
+// The file image is staged to the device once, sealed or verified there by
+// the ragged kernel in its SSTable modes, and the trailers (seal) or the
+// per-block flags (verify) come back.
+#include "../../include/lsbm/table_checksum.h"
+
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+
+#include "../../include/lsbm_crc32c.h"
+
+namespace lsbm {
+
+std::string Status::ToString() const {
+  switch (code_) {
+    case kOk: return "OK";
+    case kCorruption: return "Corruption: " + msg_;
+    case kInvalidArgument: return "Invalid argument: " + msg_;
+    default: return "IO error: " + msg_;
+  }
+}
+
+std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64_t* file_size) {
+  std::vector<BlockHandle> h(sizes.size());
+  uint64_t off = 0;
+  for (size_t i = 0; i < sizes.size(); i++) {
+    h[i] = BlockHandle{off, sizes[i]};
+    off += sizes[i] + kBlockTrailerSize;
+  }
+  if (file_size) *file_size = off;
+  return h;
+}
+
+namespace {
+
+struct DeviceBuffers {
+  uint8_t* file = nullptr;
+  uint64_t* handles = nullptr;
+  uint8_t* aux = nullptr;   // types (seal) or ok flags (verify)
+  uint32_t* nbad = nullptr;
+  ~DeviceBuffers() {
+    if (file) (void)hipFree(file);
+    if (handles) (void)hipFree(handles);
+    if (aux) (void)hipFree(aux);
+    if (nbad) (void)hipFree(nbad);
+  }
+};
+
+Status hip_status(hipError_t e, const char* what) {
+  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+Status check_handles(size_t file_size, const BlockHandle* h, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (h[i].offset > file_size || h[i].size > file_size - h[i].offset ||
+        file_size - h[i].offset - h[i].size < kBlockTrailerSize)
+      return Status::Corruption("truncated block read");  // table/format.cc:88-91
+  return Status::OK();
+}
+
+// Stage file + handles (+ aux bytes) on `device`.
+Status stage(int device, const void* file, size_t file_size, const BlockHandle* h, size_t n,
+             const uint8_t* aux_in, DeviceBuffers* d) {
+  int rc = lsbm_crc32c_init(device);
+  if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&d->file, file_size ? file_size : 1);
+  if (e == hipSuccess) e = hipMalloc(&d->handles, n * sizeof(BlockHandle));
+  if (e == hipSuccess) e = hipMalloc(&d->aux, n);
+  if (e == hipSuccess) e = hipMalloc(&d->nbad, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(d->file, file, file_size, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(d->handles, h, n * sizeof(BlockHandle), hipMemcpyHostToDevice);  // {offset,size}
+  if (e == hipSuccess && aux_in) e = hipMemcpy(d->aux, aux_in, n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(d->nbad, 0, sizeof(uint32_t));
+  return e == hipSuccess ? Status::OK() : hip_status(e, "staging");
+}
+
+}  // namespace
+
+Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
+                  const uint8_t* types, size_t n) {
+  if (n == 0) return Status::OK();
+  if (!file || !handles || !types) return Status::InvalidArgument("null pointer");
+  Status s = check_handles(file_size, handles, n);
+  if (!s.ok()) return s;
+  DeviceBuffers d;
+  s = stage(device, file, file_size, handles, n, types, &d);
+  if (!s.ok()) return s;
+  if (lsbm_sst_seal_dev(d.file, d.handles, d.aux, n, nullptr) != LSBM_OK)
+    return Status::IOError(lsbm_crc32c_last_error());
+  hipError_t e = hipDeviceSynchronize();
+  // bring back only the trailers
+  for (size_t i = 0; e == hipSuccess && i < n; i++) {
+    const uint64_t t = handles[i].offset + handles[i].size;
+    e = hipMemcpyAsync(file + t, d.file + t, kBlockTrailerSize, hipMemcpyDeviceToHost, nullptr);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return e == hipSuccess ? Status::OK() : hip_status(e, "seal");
+}
+
+Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
+                    size_t n, std::vector<uint8_t>* ok) {
+  if (ok) ok->assign(n, 1);
+  if (n == 0) return Status::OK();
+  if (!file || !handles) return Status::InvalidArgument("null pointer");
+  Status s = check_handles(file_size, handles, n);
+  if (!s.ok()) return s;
+  DeviceBuffers d;
+  s = stage(device, file, file_size, handles, n, nullptr, &d);
+  if (!s.ok()) return s;
+  if (lsbm_sst_verify_dev(d.file, d.handles, n, d.aux, d.nbad, nullptr) != LSBM_OK)
+    return Status::IOError(lsbm_crc32c_last_error());
+  uint32_t nbad = 0;
+  hipError_t e = hipMemcpy(&nbad, d.nbad, sizeof(nbad), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && ok) e = hipMemcpy(ok->data(), d.aux, n, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_status(e, "verify");
+  return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
+}
+
+}  // namespace lsbm

@@ -1,0 +1,82 @@
+// C++ host-side parity test of the batched SSTable trailer seal / verify
+// (include/lsbm/table_checksum.h) against the per-block reference pattern of
+// TableBuilder::WriteRawBlock (table/table_builder.cc:245-249) and ReadBlock
+// (table/format.cc:95-103), computed with util/crc32c.h.  Needs a GPU.
+#include <stdio.h>
+#include <string.h>
+
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "lsbm/table_checksum.h"
+#include "util/crc32c.h"
+
+static int fails = 0;
+#define EXPECT(c)                                          \
+  do {                                                     \
+    if (!(c)) {                                            \
+      printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);   \
+      fails++;                                             \
+    }                                                      \
+  } while (0)
+
+static void encode_fixed32(char* p, uint32_t v) {
+  for (int k = 0; k < 4; k++) p[k] = (char)(v >> (8 * k));
+}
+
+int main() {
+  std::mt19937_64 rng(20261015);
+  const size_t n = 3000;
+  std::vector<uint64_t> sizes(n);
+  for (auto& s : sizes) s = rng() % 9000;
+  sizes[0] = 0;
+  sizes[1] = 4118;  // a db_bench-sized data block
+  uint64_t file_size = 0;
+  std::vector<lsbm::BlockHandle> h = lsbm::LayoutBlocks(sizes, &file_size);
+  std::string file(file_size, '\0');
+  for (size_t i = 0; i < n; i++)
+    for (uint64_t k = 0; k < sizes[i]; k++) file[h[i].offset + k] = (char)(' ' + rng() % 95);
+  std::vector<uint8_t> types(n);
+  for (auto& t : types) t = rng() & 1 ? lsbm::kSnappyCompression : lsbm::kNoCompression;
+
+  lsbm::Status s = lsbm::SealBlocks(0, &file[0], file.size(), h.data(), types.data(), n);
+  EXPECT(s.ok());
+  // reference pattern, one block at a time
+  for (size_t i = 0; i < n; i++) {
+    const char* block = file.data() + h[i].offset;
+    char trailer[5];
+    trailer[0] = (char)types[i];
+    uint32_t crc = leveldb::crc32c::Value(block, sizes[i]);
+    crc = leveldb::crc32c::Extend(crc, trailer, 1);
+    encode_fixed32(trailer + 1, leveldb::crc32c::Mask(crc));
+    EXPECT(memcmp(trailer, block + sizes[i], 5) == 0);
+    // ReadBlock's check on what was written
+    const char* data = block;
+    uint32_t stored;
+    memcpy(&stored, data + sizes[i] + 1, 4);
+    EXPECT(leveldb::crc32c::Unmask(stored) == leveldb::crc32c::Value(data, sizes[i] + 1));
+  }
+  std::vector<uint8_t> ok;
+  s = lsbm::VerifyBlocks(0, file.data(), file.size(), h.data(), n, &ok);
+  EXPECT(s.ok());
+  // corrupt: a payload byte of block 7, the type byte of block 42, a crc byte of block 99
+  file[h[7].offset + 3] ^= 0x40;
+  file[h[42].offset + h[42].size] ^= 0x01;
+  file[h[99].offset + h[99].size + 2] ^= 0x80;
+  s = lsbm::VerifyBlocks(0, file.data(), file.size(), h.data(), n, &ok);
+  EXPECT(s.IsCorruption());
+  EXPECT(s.ToString() == "Corruption: block checksum mismatch");
+  std::set<size_t> bad;
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) bad.insert(i);
+  EXPECT((bad == std::set<size_t>{7, 42, 99}));
+  // a handle running past the end of the file
+  lsbm::BlockHandle trunc{file_size - 3, 10};
+  s = lsbm::VerifyBlocks(0, file.data(), file.size(), &trunc, 1, &ok);
+  EXPECT(s.IsCorruption() && s.ToString() == "Corruption: truncated block read");
+  printf("%s (%zu blocks, %llu bytes)\n", fails ? "FAILED" : "OK", n,
+         (unsigned long long)file_size);
+  return fails ? 1 : 0;
+}

@@ -250,3 +250,19 @@ def test_config2_full_1M_x_4KiB(torch_cuda, oracle, golden):
 
 def test_config3_full_1M_x_64KiB(torch_cuda, oracle, golden):
     _config_fixed(torch_cuda, oracle, golden, "cfg3_64k", 0x5EED0001, 65536, 1 << 20, 1 << 16)
+
+
+# ---------------------------------------------------------------- C++ host layer
+def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
+    """include/lsbm/table_checksum.h used from C++ the way table/ would."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "table_gpu_test"
+    libdir = os.path.join(repo, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(repo, "include"),
+                    os.path.join(repo, "tests", "cpp", "table_gpu_test.cc"), "-L", libdir,
+                    "-llsbm_crc32c", "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK")
