@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/lsbm_crc32c.h"
@@ -80,6 +81,9 @@ void build_consts(DevConsts* c) {
     const uint32_t q = w >> 9, nib = (w >> 5) & 15u, slot = w & 31u;
     c->lds_image[kNibFin / 4 + w] = c->fin_nib[slot & 7u][q * 16 + nib];
   }
+  for (uint32_t i = 0; i < 16; i++)  // A^(4096 * 2^i) = A^(2^(12+i))
+    memcpy(&c->lds_image[kNibU4096 / 4 + i * 128], c->pow_nib[12 + i], 512);
+  memset(c->zero16, 0, sizeof(c->zero16));
 }
 
 void init_device(int dev, DeviceState* st) {
@@ -149,8 +153,15 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
   if (rc != LSBM_OK) return rc;
   if (a.n == 0) return LSBM_OK;
   a.dc = st->d_consts;
-  hipError_t e = launch_ragged(a, grid_for(st, a.n), stream);
-  return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_ragged_kernel");
+  if (a.dbg_hi == 0) a.dbg_hi = ~0ull;  // debug-bounds builds: unknown range = unchecked
+  // per-block accumulators, stream-ordered so the call stays asynchronous
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&a.acc), a.n * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return fail_hip(e, "hipMallocAsync(acc)");
+  e = hipMemsetAsync(a.acc, 0, a.n * sizeof(uint32_t), stream);
+  if (e == hipSuccess) e = launch_ragged(a, (int)st->num_cus, stream);
+  hipError_t e2 = hipFreeAsync(a.acc, stream);
+  if (e != hipSuccess) return fail_hip(e, "crc32c_units_kernel");
+  return e2 == hipSuccess ? LSBM_OK : fail_hip(e2, "hipFreeAsync(acc)");
 }
 
 // ---- host-staged pipeline ----
@@ -163,6 +174,7 @@ struct Slot {
   uint64_t* d_off = nullptr;
   uint32_t* d_init = nullptr;
   uint32_t* d_out = nullptr;
+  uint32_t* d_acc = nullptr;
   uint64_t cap_bytes = 0, cap_blocks = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
@@ -187,8 +199,10 @@ void free_slot_buffers(Slot& s) {
   if (s.d_off) hipFree(s.d_off);
   if (s.d_init) hipFree(s.d_init);
   if (s.d_out) hipFree(s.d_out);
+  if (s.d_acc) hipFree(s.d_acc);
   s.h_data = nullptr; s.h_off = nullptr; s.h_init = nullptr; s.h_out = nullptr;
   s.d_data = nullptr; s.d_off = nullptr; s.d_init = nullptr; s.d_out = nullptr;
+  s.d_acc = nullptr;
   s.cap_bytes = s.cap_blocks = 0;
 }
 
@@ -215,9 +229,47 @@ hipError_t reserve_slot(Slot& s, uint64_t bytes, uint64_t blocks) {
   if ((e = hipMalloc(&s.d_off, (blocks + 1) * 8)) != hipSuccess) return e;
   if ((e = hipMalloc(&s.d_init, blocks * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&s.d_out, blocks * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&s.d_acc, blocks * 4)) != hipSuccess) return e;
   s.cap_bytes = bytes;
   s.cap_blocks = blocks;
   return hipSuccess;
+}
+
+// Page-locked (hipHostMalloc'd or hipHostRegister'ed) host memory can be the
+// source of an async DMA as it is; pageable memory goes through staging.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" for pageable memory
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// Copy blocks [first, last) of a pageable source into the pinned staging
+// buffer at their rebased offsets, on up to 8 threads for large chunks.
+void gather_blocks(uint8_t* dst, const uint64_t* rebased, const uint8_t* src,
+                   const uint64_t* offsets, uint64_t first, uint64_t last) {
+  auto copy_range = [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++) {
+      const uint64_t s0 = offsets[i], s1 = offsets[i + 1];
+      if (s1 > s0) memcpy(dst + rebased[i - first], src + s0, s1 - s0);
+    }
+  };
+  const uint64_t bytes = rebased[last - first];
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = bytes < (8u << 20) ? 1u : std::min(8u, hw);
+  if (nt == 1) {
+    copy_range(first, last);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t per = (last - first + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; t++) {
+    const uint64_t lo = std::min(last, first + t * per), hi = std::min(last, lo + per);
+    if (lo < hi) th.emplace_back(copy_range, lo, hi);
+  }
+  for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -252,6 +304,7 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
   const uintptr_t b = reinterpret_cast<uintptr_t>(d_base);
   const bool fast = (b % 16 == 0) && (stride % 16 == 0) && len >= kRowBytes &&
                     (len % kRowBytes == 0) && stride >= len && stride <= (1ull << 28) &&
+                    7 * stride + len < (1ull << 31) &&
                     n_blocks < (1ull << 34);
   if (fast) {
     const gf2::Mat an = gf2::byte_pow((int64_t)len);
@@ -269,6 +322,8 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
   a.len = len;
   a.extents = kExtFixed;
   a.n = n_blocks;
+  a.dbg_lo = reinterpret_cast<uint64_t>(d_base);
+  a.dbg_hi = a.dbg_lo + (n_blocks - 1) * stride + len;
   a.init = d_init;
   a.out = d_out;
   a.flags = flags;
@@ -390,6 +445,7 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
   Staging& stg = g_staging[device];
   std::lock_guard<std::mutex> lock(stg.mu);
   const uint8_t* src = static_cast<const uint8_t*>(h_base);
+  const bool src_pinned = host_pinned(h_base);
   constexpr uint64_t kChunkBytes = 64ull << 20;
   constexpr uint64_t kChunkBlocks = 1ull << 16;
   const int nslots = 3;
@@ -425,19 +481,26 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
       rc = fail_hip(e, "staging buffers");
       break;
     }
-    // gather into pinned memory with rebased offsets (16-B aligned start)
+    // rebased offsets; a chunk whose extents are in order and tight can be
+    // DMA-ed straight from a pinned source, otherwise it is gathered
+    const uint64_t cnt = last - next;
     uint64_t pos = 0;
+    bool tight = src_pinned;
     for (uint64_t i = next; i < last; i++) {
       const uint64_t s0 = h_offsets[i], s1 = h_offsets[i + 1];
       const uint64_t len = s1 > s0 ? s1 - s0 : 0;
+      if (s0 != h_offsets[next] + pos) tight = false;
       s.h_off[i - next] = pos;
-      memcpy(s.h_data + pos, src + s0, len);
       pos += len;
     }
-    s.h_off[last - next] = pos;
-    const uint64_t cnt = last - next;
+    s.h_off[cnt] = pos;
     if (h_init) memcpy(s.h_init, h_init + next, cnt * 4);
-    e = hipMemcpyAsync(s.d_data, s.h_data, pos, hipMemcpyHostToDevice, s.stream);
+    if (tight) {
+      e = hipMemcpyAsync(s.d_data, src + h_offsets[next], pos, hipMemcpyHostToDevice, s.stream);
+    } else {
+      gather_blocks(s.h_data, s.h_off, src, h_offsets, next, last);
+      e = hipMemcpyAsync(s.d_data, s.h_data, pos, hipMemcpyHostToDevice, s.stream);
+    }
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess && h_init)
@@ -455,7 +518,11 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
     a.flags = flags;
     a.mode = kModeOut;
     a.dc = st->d_consts;
-    e = launch_ragged(a, grid_for(st, cnt), s.stream);
+    a.acc = s.d_acc;
+    a.dbg_lo = reinterpret_cast<uint64_t>(s.d_data);
+    a.dbg_hi = a.dbg_lo + pos;
+    e = hipMemsetAsync(s.d_acc, 0, cnt * 4, s.stream);
+    if (e == hipSuccess) e = launch_ragged(a, (int)st->num_cus, s.stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);

@@ -2,8 +2,9 @@
 //
 // crc32c_fixed_kernel   fixed-stride, len % 128 == 0, 16-B aligned blocks
 //                       (SSTable-sized 4 KiB and 64 KiB batches; the headline)
-// crc32c_ragged_kernel  any extents, any alignment: offsets[] batches, verify,
-//                       and the SSTable trailer seal / verify modes
+// crc32c_units_kernel   any extents, any alignment (offsets[] batches, verify,
+// crc32c_finish_kernel  SSTable trailer seal / verify): 32-row units per lane
+//                       group, partial CRCs xor-ed per block, then finished
 // fill_splitmix64_kernel, stream_read_kernel   benchmark helpers
 //
 // Both CRC kernels compute, per block, exactly what lsbm's
@@ -21,6 +22,9 @@ namespace lsbm {
 __shared__ uint32_t g_lds[kLdsWords];
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Global-address-space pointer: addresses built from integers would otherwise
+// be generic (flat) loads, which count on lgkmcnt too and force full drains.
+typedef const __attribute__((address_space(1))) u32x4* gptr_u32x4;
 
 #ifdef LSBM_DIAG_STAMPS  // diagnostic builds only (tools/ablate.sh): per-wave timeline
 __device__ uint64_t g_stamps[4][65536];  // start, first-data, end, xcc id
@@ -100,9 +104,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     // wave-uniform descriptor over the group's 8 blocks; per-lane 32-bit
     // offset (host guarantees 8 * stride < 2^32).  Lanes past the end re-read
     // block 0 of the group and discard the result.
+    // num_records = the bytes of this group's blocks that exist: a load past
+    // them returns zeros instead of touching memory beyond the batch
+    const uint64_t nb = n_blocks - grp * 8 < 8 ? n_blocks - grp * 8 : 8;
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + grp * 8 * stride),
-                                             (short)0, (int)0x7fffffff, 0x00020000);
+                                             (short)0, (int)((nb - 1) * stride + rows * kRowBytes),
+                                             0x00020000);
     loff = (blk < n_blocks ? g : 0u) * (uint32_t)stride + 16u * li;
+    asm volatile("" : "+v"(loff));  // defined in every lane (see crc32c_units_kernel)
   };
   // Static interleave: wave w takes groups w, w + nwaves, ...  At any moment
   // the GPU streams one contiguous ~128 MiB window of the batch.  (A dynamic
@@ -170,14 +179,21 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 #endif
 }
 // ---------------------------------------------------------------------------
-// Ragged kernel.  Same row/braid machinery, but rows are 128-B aligned in the
-// absolute address space, so every load is an aligned 16-B load whatever the
-// block's alignment.  For block [s, e):
+// Ragged path: units kernel + finish kernel.
+//
+// Frame.  Rows are 128-B aligned in the absolute address space, so every load
+// is an aligned 16-B load whatever the block's alignment.  For block [s, e):
 //   * bytes of the frame outside [s, e) are zero; leading zeros leave a raw
 //     CRC unchanged, so the frame may start early for free;
 //   * the init register v = init ^ ~0 is injected as 4 virtual bytes
 //     u = A^-4(v) at [s-4, s) (absorbing u from zero gives exactly v);
 //   * the frame ends z = frame_end - e bytes late: undone with A^-z.
+// Units.  The frame is cut into units of <= 32 rows (crc32c_types.h).  Each
+// wave walks a contiguous range of blocks and hands the next 8 units of the
+// range to its 8 lane groups, so most steps are uniform 32-row loops whatever
+// the block lengths.  A unit's raw CRC, shifted to the frame end by
+// A^(4096 k), is xor-ed into acc[block]; the finish kernel turns acc into
+// the CRC and applies the output mode.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t frame_word(uint32_t raw, uint64_t a, uint64_t s, uint64_t e,
                                                uint32_t u) {
@@ -194,7 +210,59 @@ __device__ __forceinline__ uint32_t frame_word(uint32_t raw, uint64_t a, uint64_
   return w;
 }
 
-__global__ __launch_bounds__(kBlockThreads) void crc32c_ragged_kernel(RaggedArgs args) {
+// Block b's extent [s, e) as absolute addresses.
+__device__ __forceinline__ void block_extent(const RaggedArgs& a, uint64_t b, uint64_t& s,
+                                             uint64_t& e) {
+  const uint64_t base = reinterpret_cast<uint64_t>(a.base);
+  if (a.extents == kExtHandles) {
+    const uint64_t off = a.handles[2 * b], sz = a.handles[2 * b + 1];
+    s = base + off;
+    e = s + sz + (a.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
+  } else if (a.extents == kExtFixed) {
+    s = base + b * a.stride;
+    e = s + a.len;
+  } else {
+    s = base + a.offsets[b];
+    e = base + a.offsets[b + 1];
+    if (e < s) e = s;
+  }
+}
+
+struct Frame {
+  uint64_t s, e, row0, rows;  // rows >= 1
+  uint32_t units;             // ceil(rows / 32)
+};
+
+__device__ __forceinline__ Frame block_frame(const RaggedArgs& a, uint64_t b) {
+  Frame f;
+  block_extent(a, b, f.s, f.e);
+  f.row0 = (f.s - 4) >> 7;
+  const uint64_t row_end = (f.e + 127) >> 7;
+  f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
+  f.units = (uint32_t)((f.rows + kUnitRows - 1) / kUnitRows);
+  return f;
+}
+
+// M(v) for nibble tables in LDS at byte offset `tab` (low 6 bits clear).
+__device__ __forceinline__ uint32_t nib_lds_at(const uint32_t* lds, uint32_t tab, uint32_t v) {
+  uint32_t t[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t f = q == 0 ? (v << 2) : (v >> (4 * q - 2));
+    t[q] = lds_load(lds, ((f & 0x3cu) | tab) + q * 64);
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// A^(4096 k)(v): LDS tables for bits 0..15 of k, global ones beyond.
+__device__ __forceinline__ uint32_t shift_units(const uint32_t* lds, const DevConsts* dc,
+                                                uint32_t v, uint64_t k) {
+  for (uint32_t i = 0; k; i++, k >>= 1)
+    if (k & 1u) v = i < 16 ? nib_lds_at(lds, kNibU4096 + i * 512, v) : nib_glb(dc->pow_nib[12 + i], v);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
   const DevConsts* __restrict__ dc = args.dc;
   load_lds_tables(g_lds, dc);
   const uint32_t lane = threadIdx.x & 63u;
@@ -202,89 +270,178 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_ragged_kernel(RaggedArgs
   const uint32_t lb = (lane & 31u) << 2;
   const uint32_t L0 = lb, L1 = lb | 0x80u, L2 = lb | 0x10000u, L3 = lb | 0x10080u;
   const uint32_t lane_fin = kNibFin | lb;
-  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg + (threadIdx.x >> 6);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
-  const uint64_t ngroups = (args.n + 7) / 8;
-  const uint64_t base_addr = reinterpret_cast<uint64_t>(args.base);
+  // this wave's contiguous range of blocks
+  const uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
+  const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
+#ifdef LSBM_DEBUG_BOUNDS
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    printf("units: n %lu base %lx dbg [%lx, %lx) acc %p dc %p dummy %lx grid %u\n", (unsigned long)args.n,
+           (unsigned long)args.base, (unsigned long)args.dbg_lo, (unsigned long)args.dbg_hi, args.acc, dc,
+           (unsigned long)dummy, gridDim.x);
+#endif
 
-  for (uint64_t grp = wave; grp < ngroups; grp += nwaves) {
-    const uint64_t blk = grp * 8 + g;
-    const bool valid = blk < args.n;
-    uint64_t s = base_addr, e = base_addr;
-    if (valid) {
-      if (args.extents == kExtHandles) {
-        const uint64_t off = args.handles[2 * blk], sz = args.handles[2 * blk + 1];
-        s = base_addr + off;
-        e = s + sz + (args.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
-      } else if (args.extents == kExtFixed) {
-        s = base_addr + blk * args.stride;
-        e = s + args.len;
-      } else {
-        s = base_addr + args.offsets[blk];
-        e = base_addr + args.offsets[blk + 1];
-        if (e < s) e = s;
+  // wave cursor: unit ordinal `cur_o` of block `cur_b` is the next unassigned unit
+  uint64_t cur_b = b_lo;
+  uint32_t cur_o = 0;
+  while (cur_b < b_hi) {
+    // this group's unit: walk forward g units from the cursor
+    uint64_t b = cur_b;
+    uint32_t o = cur_o + g;
+    Frame f = {0, 0, 0, 1, 1};  // defined on every path (idle lanes read it too)
+    bool active = false;
+    while (b < b_hi) {
+      f = block_frame(args, b);
+      if (o < f.units) { active = true; break; }
+      o -= f.units;
+      b++;
+    }
+    uint32_t rows = 0, k = 0;
+    uint64_t row_a = 0;  // absolute address of this lane's slice of the unit's first row
+    bool edge = false;
+    uint32_t u = 0;
+    if (active) {
+      const uint32_t first_rows = (uint32_t)(f.rows - (uint64_t)kUnitRows * (f.units - 1));
+      rows = o == 0 ? first_rows : kUnitRows;
+      const uint64_t r0 = f.row0 + (o == 0 ? 0 : first_rows + (uint64_t)kUnitRows * (o - 1));
+      row_a = r0 * kRowBytes + 16u * li;
+      k = f.units - 1 - o;
+      // a unit needs masking when its span reaches outside [s, e) (the frame
+      // start with the init bytes, the frame end, or a unit that starts in
+      // the row holding s when the short first unit is a single row)
+      edge = r0 * kRowBytes < f.s || (r0 + rows) * kRowBytes > f.e;
+      if (r0 * kRowBytes < f.s) {  // the init bytes [s-4, s) may straddle two units
+        const uint32_t v = (args.init ? args.init[b] : 0u) ^ 0xffffffffu;
+        u = nib_glb(dc->neg4_nib, v);
       }
     }
-    const uint32_t v = (args.init && valid ? args.init[blk] : 0u) ^ 0xffffffffu;
-    const uint32_t u = nib_glb(dc->neg4_nib, v);
-    const uint64_t row0 = (s - 4) >> 7;
-    const uint64_t row_end = (e + 127) >> 7;  // one past the last row
-    const uint64_t rows = row_end > row0 ? row_end - row0 : 1;
-    const uint32_t z = (uint32_t)((row0 + rows) * kRowBytes - e);
+    // uniform trip count: the longest unit of the 8 groups
+    uint32_t rows_max = rows;
+    rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 8));
+    rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 16));
+    rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 32));
+    rows_max = __builtin_amdgcn_readfirstlane(rows_max);
 
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // A^128(0) = 0: row 0 needs no special case
-    for (uint64_t r = 0; r < rows; r++) {
-      const uint64_t a = (row0 + r) * kRowBytes + 16u * li;
-      u32x4 w = {0u, 0u, 0u, 0u};
-      if (a + 16 > s - 4 && a < e) {
-        if (s < e && a + 16 > s && a < e) w = *reinterpret_cast<const u32x4*>(a);
-        if (a < s || a + 16 > e) {
-          w.x = frame_word(w.x, a, s, e, u);
-          w.y = frame_word(w.y, a + 4, s, e, u);
-          w.z = frame_word(w.z, a + 8, s, e, u);
-          w.w = frame_word(w.w, a + 12, s, e, u);
-        }
+    // A safe load address for every lane and row: rows past this unit, idle
+    // lanes and edge chunks wholly outside [s, e) read the zero pad instead.
+    // Branch-free on purpose (bitwise & |): with short-circuit && / || the
+    // structurizer turned the select below into control flow and lost the
+    // pad address for lanes whose value is dead -- they then loaded from
+    // their raw row address (observed: reads below the batch, a GPU fault).
+    auto row_ok = [&](uint32_t r) -> bool {
+      const uint64_t a = row_a + (uint64_t)r * kRowBytes;
+      const bool inside = (a + 16 > f.s) & (a < f.e) & (f.s < f.e);
+      return (r < rows) & ((!edge) | inside);
+    };
+    auto row_addr = [&](uint32_t r) -> gptr_u32x4 {
+      uint64_t p = row_ok(r) ? row_a + (uint64_t)r * kRowBytes : dummy;
+      asm volatile("" : "+v"(p));  // materialise the per-lane address before the load
+#ifdef LSBM_DEBUG_BOUNDS  // diagnostic builds only: report and neutralise wild loads
+      if (p != dummy && (p + 16 <= args.dbg_lo || p >= args.dbg_hi)) {
+        printf("OOB wave %lu lane %u b %lu o %u r %u rows %u edge %d s %lx e %lx row_a %lx p %lx\n",
+               (unsigned long)wave, lane, (unsigned long)b, o, r, rows, (int)edge,
+               (unsigned long)f.s, (unsigned long)f.e, (unsigned long)row_a, (unsigned long)p);
+        p = dummy;
       }
-      STEP_ROW(w);
+#endif
+      return reinterpret_cast<gptr_u32x4>(p);
+    };
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    auto absorb = [&](u32x4 w, uint32_t r) {  // rows read from the pad are zero
+      const uint64_t a = row_a + (uint64_t)r * kRowBytes;
+      if (edge && (a < f.s || a + 16 > f.e)) {
+        w.x = frame_word(w.x, a, f.s, f.e, u);
+        w.y = frame_word(w.y, a + 4, f.s, f.e, u);
+        w.z = frame_word(w.z, a + 8, f.s, f.e, u);
+        w.w = frame_word(w.w, a + 12, f.s, f.e, u);
+      }
+      if (r < rows) STEP_ROW(w);
+    };
+    // two banks of 4 rows, loads always issued (pad reads past the unit) so
+    // that the loads in flight are counted exactly
+    u32x4 ba[4], bb[4];
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(k2));
+    for (uint32_t r = 0; r < rows_max; r += 8) {
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) bb[k2] = __builtin_nontemporal_load(row_addr(r + 4 + k2));
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(ba[k2], r + k2);
+      if (r + 4 >= rows_max) break;
+      if (r + 8 < rows_max) {
+#pragma unroll
+        for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(r + 8 + k2));
+      }
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(bb[k2], r + 4 + k2);
     }
-    const uint32_t padded = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
-    if (li == 7u && valid) {
-      uint32_t l = nib_glb(dc->neg_nib[z], padded);  // register after the block
-      if (args.mode == kModeSstSeal) {
-        const uint8_t typ = args.types[blk];
-        l = dc->t0[(l ^ typ) & 0xffu] ^ (l >> 8);  // Extend(crc, &type, 1)
+    const uint32_t raw = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+    if (active) {
+      const uint32_t contrib = shift_units(g_lds, dc, raw, k);
+#ifdef LSBM_DEBUG_BOUNDS
+      if (li == 0 && b >= args.n) printf("ACC OOB wave %lu b %lu n %lu\n", (unsigned long)wave, (unsigned long)b, (unsigned long)args.n);
+      else
+#endif
+      if (li == 0) atomicXor(args.acc + b, contrib);
+    }
+    // advance the cursor by 8 units (uniform: every lane walks the same path)
+    cur_o += 8;
+    while (cur_b < b_hi) {
+      const uint32_t m = block_frame(args, cur_b).units;
+      if (cur_o < m) break;
+      cur_o -= m;
+      cur_b++;
+    }
+  }
+}
+
+// One thread per block: acc -> CRC -> output mode.
+__global__ __launch_bounds__(256) void crc32c_finish_kernel(RaggedArgs args) {
+  const DevConsts* __restrict__ dc = args.dc;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < args.n;
+       b += (uint64_t)gridDim.x * blockDim.x) {
+    const Frame f = block_frame(args, b);
+    const uint32_t z = (uint32_t)((f.row0 + f.rows) * kRowBytes - f.e);
+#ifdef LSBM_DEBUG_BOUNDS
+    if (z >= 128) { printf("Z OOB b %lu z %u s %lx e %lx row0 %lx rows %lu\n", (unsigned long)b, z, (unsigned long)f.s, (unsigned long)f.e, (unsigned long)f.row0, (unsigned long)f.rows); continue; }
+#endif
+    uint32_t l = nib_glb(dc->neg_nib[z], args.acc[b]);  // register after the block
+    if (args.mode == kModeSstSeal) {
+      const uint8_t typ = args.types[b];
+      l = dc->t0[(l ^ typ) & 0xffu] ^ (l >> 8);  // Extend(crc, &type, 1)
+    }
+    const uint32_t crc = l ^ 0xffffffffu;
+    switch (args.mode) {
+      case kModeOut:
+        args.out[b] = (args.flags & 1u) ? mask_crc(crc) : crc;
+        break;
+      case kModeVerify: {
+        const uint32_t got = (args.flags & 1u) ? mask_crc(crc) : crc;
+        const bool good = got == args.expect[b];
+        args.ok[b] = good ? 1 : 0;
+        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
+        break;
       }
-      const uint32_t crc = l ^ 0xffffffffu;
-      switch (args.mode) {
-        case kModeOut:
-          args.out[blk] = (args.flags & 1u) ? mask_crc(crc) : crc;
-          break;
-        case kModeVerify: {
-          const uint32_t got = (args.flags & 1u) ? mask_crc(crc) : crc;
-          const bool good = got == args.expect[blk];
-          args.ok[blk] = good ? 1 : 0;
-          if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-          break;
-        }
-        case kModeSstSeal: {
-          uint8_t* t = args.file + (e - base_addr);
-          const uint32_t m = mask_crc(crc);
-          t[0] = args.types[blk];
-          t[1] = (uint8_t)m;
-          t[2] = (uint8_t)(m >> 8);
-          t[3] = (uint8_t)(m >> 16);
-          t[4] = (uint8_t)(m >> 24);
-          break;
-        }
-        default: {  // kModeSstVerify: table/format.cc:95-103
-          const uint8_t* t = reinterpret_cast<const uint8_t*>(e);
-          const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) |
-                                  ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
-          const bool good = unmask_crc(stored) == crc;
-          args.ok[blk] = good ? 1 : 0;
-          if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-          break;
-        }
+      case kModeSstSeal: {  // table/table_builder.cc:245-249
+        uint8_t* t = args.file + (f.e - reinterpret_cast<uint64_t>(args.base));
+        const uint32_t m = mask_crc(crc);
+        t[0] = args.types[b];
+        t[1] = (uint8_t)m;
+        t[2] = (uint8_t)(m >> 8);
+        t[3] = (uint8_t)(m >> 16);
+        t[4] = (uint8_t)(m >> 24);
+        break;
+      }
+      default: {  // kModeSstVerify: table/format.cc:95-103
+        const uint8_t* t = reinterpret_cast<const uint8_t*>(f.e);
+        const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) |
+                                ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+        const bool good = unmask_crc(stored) == crc;
+        args.ok[b] = good ? 1 : 0;
+        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
+        break;
       }
     }
   }
@@ -373,8 +530,14 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
   return hipGetLastError();
 }
 
+// acc must hold n zeroed words.
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32c_ragged_kernel, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+  hipLaunchKernelGGL(crc32c_units_kernel, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t fin_wgs = (a.n + 255) / 256;
+  hipLaunchKernelGGL(crc32c_finish_kernel, dim3((unsigned)(fin_wgs < 65536 ? fin_wgs : 65536)),
+                     dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -17,7 +17,8 @@ constexpr uint32_t kLdsByteTabBytes = 131072;
 constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
 constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
                                          // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
-constexpr uint32_t kLdsBytes = kNibFin + 8 * 16 * 32 * 4;
+constexpr uint32_t kNibU4096 = kNibFin + 8 * 16 * 32 * 4;  // A^(4096 * 2^i), i = 0..15
+constexpr uint32_t kLdsBytes = kNibU4096 + 16 * 512;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
 // Tables in device global memory, built once per device by the host (gf2.h).
@@ -31,6 +32,7 @@ struct DevConsts {
   // The kernels' LDS image, prebuilt by the host so that each workgroup
   // fills its LDS with ~9 coalesced 16-B loads per thread.
   alignas(16) uint32_t lds_image[kLdsWords];
+  alignas(16) uint32_t zero16[4];  // a safe load target for idle lanes
 };
 
 // How the ragged kernel finds block i's extent [s, e).
@@ -46,6 +48,12 @@ enum RaggedMode : uint32_t {
   kModeSstSeal = 2,    // write trailer [type][Mask(crc(block || type))] after the block
   kModeSstVerify = 3,  // ok[i] = stored trailer == Mask(crc(block || type))
 };
+
+// Ragged path: a block's 128-B-aligned frame [row0, row_end) is cut into
+// units of at most kUnitRows rows: ordinal 0 is the (possibly short) unit at
+// the frame start, ordinals 1..m-1 are full units.  A unit's raw CRC is
+// shifted to the frame end with A^(4096 * k), k = m - 1 - ordinal.
+constexpr uint32_t kUnitRows = 32;
 
 struct RaggedArgs {
   const uint8_t* base;      // extents are byte offsets from here
@@ -64,6 +72,8 @@ struct RaggedArgs {
   uint32_t mode;
   uint32_t extents;
   const DevConsts* dc;
+  uint32_t* acc;         // n per-block accumulators (zeroed before the units kernel)
+  uint64_t dbg_lo, dbg_hi;  // LSBM_DEBUG_BOUNDS builds: the valid data range
 };
 
 }  // namespace lsbm

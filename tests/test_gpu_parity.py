@@ -266,3 +266,21 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")
+
+
+def test_host_staged_pinned_source_and_chunking(torch_cuda, oracle):
+    """A page-locked source is DMA-ed directly (no gather); > 64 MiB spans chunks."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 70000, size=3000)
+    offs = np.zeros(3001, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    total = int(offs[-1])
+    src = torch.empty(total + 7, dtype=torch.uint8, pin_memory=True)
+    h = src.numpy()
+    h[:] = stream_bytes(78, 0, total + 7)
+    view = h[7:]  # odd start inside the pinned allocation
+    got = engine.crc32c_batch_host(view, offs, masked=True)
+    want = oracle.batch_offsets(view, offs, masked=True)
+    assert np.array_equal(got, want)

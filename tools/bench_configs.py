@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Secondary measurements: configs 3 and 4 of BASELINE.json and the
+host-staged (PCIe-inclusive) rate.  One JSON line per measurement.
+
+  config3   1M x 64 KiB device-resident blocks (fixed-stride kernel)
+  config4   10M blocks, n = min(65536, 512*r + u), r ~ Zipf(0.99) over 1..128,
+            u ~ U[0, 511], densely packed at arbitrary alignment (ragged path)
+  host      host-staged batches: pinned host buffer -> GPU -> 4 B/block back
+
+Lengths are drawn from splitmix64 streams (seed 0x5EED0002), not the survey's
+mt19937_64, so that numpy regenerates them bit for bit; bytes are the on-device
+splitmix64 stream (seeds 0x5EED0001 / 0x5EED0003).  Every run spot-checks
+sampled blocks against the oracle.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from golden.splitmix import splitmix64, stream_bytes  # noqa: E402
+
+HBM = 8000.0
+
+
+def zipf_lengths(n, seed=0x5EED0002, ranks=128, theta=0.99):
+    """n = min(65536, 512*r + u): r ~ Zipf(theta) on 1..ranks, u ~ U[0, 511]."""
+    w = 1.0 / np.arange(1, ranks + 1, dtype=np.float64) ** theta
+    cdf = np.cumsum(w) / w.sum()
+    idx = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        a = splitmix64(np.uint64(seed) + 2 * idx)
+        b = splitmix64(np.uint64(seed) + 2 * idx + np.uint64(1))
+    u01 = (a >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    r = np.searchsorted(cdf, u01, side="right") + 1
+    u = (b % np.uint64(512)).astype(np.int64)
+    return np.minimum(65536, 512 * r + u).astype(np.int64)
+
+
+def time_launches(fn, stream, reps=10, warm=2):
+    import torch
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def oracle():
+    from conftest import Oracle
+    return Oracle(os.path.join(REPO, "oracle", "liboracle_crc32c.so"))
+
+
+def config3(args):
+    import torch
+    from lsbm_amd import engine
+    n, L, seed = args.c3_blocks, 65536, 0x5EED0001
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, seed)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    t = time_launches(lambda: engine.crc32c_fixed(d, L, L, n, out=out, stream=s), s)
+    got = out.cpu().numpy().view(np.uint32)
+    o = oracle()
+    rng = np.random.default_rng(3)
+    bad = sum(int(got[b] != o.value(stream_bytes(seed, int(b) * L, L).tobytes()))
+              for b in rng.choice(n, 64, replace=False))
+    gbps = n * L / t / 1e9
+    print(json.dumps({"config": "config3", "blocks": n, "block_bytes": L, "ms": round(t * 1e3, 3),
+                      "GiBps": round(n * L / t / 2**30, 1), "GBps": round(gbps, 1),
+                      "pct_hbm_peak": round(100 * gbps / HBM, 2), "sample_mismatches": bad}),
+          flush=True)
+    del d
+
+
+def config4(args):
+    import torch
+    from lsbm_amd import engine
+    n = args.c4_blocks
+    lens = zipf_lengths(n)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    start_pad = 5  # dense packing at an arbitrary alignment
+    offs += start_pad
+    total = int(offs[-1]) + 16
+    seed = 0x5EED0003
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, seed)
+    do = torch.from_numpy(offs).to("cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    t = time_launches(lambda: engine.crc32c_batch(d, do, out=out, stream=s), s, reps=5, warm=1)
+    got = out.cpu().numpy().view(np.uint32)
+    o = oracle()
+    rng = np.random.default_rng(4)
+    bad = 0
+    for b in rng.choice(n, 64, replace=False):
+        blk = stream_bytes(seed, int(offs[b]), int(lens[b])).tobytes()
+        bad += int(got[b] != o.value(blk))
+    payload = int(lens.sum())
+    gbps = payload / t / 1e9
+    print(json.dumps({"config": "config4", "blocks": n, "payload_GiB": round(payload / 2**30, 2),
+                      "mean_len": round(float(lens.mean()), 1),
+                      "frac_le_4k": round(float((lens <= 4096).mean()), 3),
+                      "ms": round(t * 1e3, 3), "GiBps": round(payload / t / 2**30, 1),
+                      "GBps": round(gbps, 1), "pct_hbm_peak": round(100 * gbps / HBM, 2),
+                      "sample_mismatches": bad}), flush=True)
+    del d, do
+
+
+def host_staged(args):
+    import torch
+    from lsbm_amd import engine
+    n, L = args.host_blocks, 4096
+    # pinned host source (hipHostMalloc via torch), bytes of the config-2 stream
+    src = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    src.numpy()[:] = stream_bytes(0x5EED0000, 0, n * L)
+    offs = np.arange(0, (n + 1) * L, L, dtype=np.uint64)
+    h = src.numpy()
+    engine.crc32c_batch_host(h[:L * 1024], offs[:1025])  # warm: staging buffers
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        got = engine.crc32c_batch_host(h, offs)
+    t = (time.perf_counter() - t0) / reps
+    o = oracle()
+    bad = sum(int(got[b] != o.value(h[b * L:(b + 1) * L].tobytes())) for b in range(0, n, n // 64))
+    print(json.dumps({"config": "host_staged", "blocks": n, "block_bytes": L,
+                      "s": round(t, 4), "GiBps": round(n * L / t / 2**30, 2),
+                      "GBps": round(n * L / t / 1e9, 2), "sample_mismatches": bad,
+                      "note": "pinned source; includes host gather into staging, H2D, kernel, "
+                              "4 B/block D2H"}), flush=True)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("which", nargs="*", default=["config3", "config4", "host"])
+    p.add_argument("--c3-blocks", type=int, default=1 << 20)
+    p.add_argument("--c4-blocks", type=int, default=10_000_000)
+    p.add_argument("--host-blocks", type=int, default=1 << 18)
+    args = p.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from lsbm_amd import engine
+    engine.init(0)
+    for w in args.which:
+        {"config3": config3, "config4": config4, "host": host_staged}[w](args)
+
+
+if __name__ == "__main__":
+    main()
