@@ -287,20 +287,47 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   uint64_t cur_b = b_lo;
   uint32_t cur_o = 0;
   while (cur_b < b_hi) {
-    // this group's unit: walk forward g units from the cursor
-    uint64_t b = cur_b;
-    uint32_t o = cur_o + g;
-    Frame f = {0, 0, 0, 1, 1};  // defined on every path (idle lanes read it too)
-    bool active = false;
-    while (b < b_hi) {
-      f = block_frame(args, b);
-      if (o < f.units) { active = true; break; }
-      o -= f.units;
-      b++;
+    // Find the 8 groups' units in one round: lane j reads block cur_b + j
+    // (8 units never span more than 9 blocks), an inclusive prefix sum over
+    // the lanes' unit counts, then one ballot per group.
+    const uint64_t bj = cur_b + lane;
+    Frame fj = {0, 0, 0, 1, 0};
+    if (lane < 9 && bj < b_hi) fj = block_frame(args, bj);
+    uint32_t pre = fj.units;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {  // lanes >= 9 contribute 0: a 16-lane scan suffices
+      const uint32_t t = (uint32_t)__shfl_up((int)pre, d, 16);
+      if ((lane & 15u) >= d) pre += t;
     }
+    const uint32_t my_t = cur_o + g;  // this group's unit, as an offset from the cursor
+    uint32_t jg = 0, jnext = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 9; q++) {
+      // count of lanes (among the first 9) whose prefix <= cur_o + q
+      const uint64_t m = __ballot((lane < 9) && pre <= cur_o + q);
+      const uint32_t c = (uint32_t)__builtin_popcountll(m);
+      if (q == g) jg = c;
+      if (q == 8) jnext = c;
+    }
+    // shuffles run with every lane active (a bpermute from an inactive
+    // source lane reads 0), then select
+    const uint32_t pre_prev = (uint32_t)__shfl((int)pre, (int)(jg ? jg - 1 : 0));
+    const uint32_t pre_before = jg ? pre_prev : 0u;
+    const uint64_t b = cur_b + jg;
+    const bool active = jg < 9 && b < b_hi;
+    Frame f = {0, 0, 0, 1, 1};
+    f.s = __shfl((unsigned long long)fj.s, (int)jg);
+    f.e = __shfl((unsigned long long)fj.e, (int)jg);
+    f.row0 = __shfl((unsigned long long)fj.row0, (int)jg);
+    f.rows = __shfl((unsigned long long)fj.rows, (int)jg);
+    f.units = (uint32_t)__shfl((int)fj.units, (int)jg);
+    const uint32_t o = my_t - pre_before;
+
     uint32_t rows = 0, k = 0;
-    uint64_t row_a = 0;  // absolute address of this lane's slice of the unit's first row
-    bool edge = false;
+    uint64_t row_a = dummy;  // absolute address of this lane's slice of the unit's first row
+    // rows whose loads are inside [s, e): [r_lo, r_hi); rows needing the
+    // masking / init-byte fix: rs0, rs1 (around s) and re (holding e - 1)
+    uint32_t r_lo = 0, r_hi = 0, rs0 = ~0u, rs1 = ~0u, re = ~0u;
     uint32_t u = 0;
     if (active) {
       const uint32_t first_rows = (uint32_t)(f.rows - (uint64_t)kUnitRows * (f.units - 1));
@@ -308,10 +335,25 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       const uint64_t r0 = f.row0 + (o == 0 ? 0 : first_rows + (uint64_t)kUnitRows * (o - 1));
       row_a = r0 * kRowBytes + 16u * li;
       k = f.units - 1 - o;
-      // a unit needs masking when its span reaches outside [s, e) (the frame
-      // start with the init bytes, the frame end, or a unit that starts in
-      // the row holding s when the short first unit is a single row)
-      edge = r0 * kRowBytes < f.s || (r0 + rows) * kRowBytes > f.e;
+      const bool edge = r0 * kRowBytes < f.s || (r0 + rows) * kRowBytes > f.e;
+      r_hi = rows;
+      if (edge) {
+        r_lo = r_hi = 0;
+        if (f.s < f.e) {
+          const int64_t dl = (int64_t)f.s - 16 - (int64_t)row_a;  // chunk end > s
+          const int64_t dh = (int64_t)f.e - (int64_t)row_a;       // chunk start < e
+          const int64_t lo = dl < 0 ? 0 : dl / (int64_t)kRowBytes + 1;
+          const int64_t hi = dh <= 0 ? 0 : (dh + kRowBytes - 1) / (int64_t)kRowBytes;
+          r_lo = (uint32_t)(lo < (int64_t)rows ? lo : rows);
+          r_hi = (uint32_t)(hi < (int64_t)rows ? hi : rows);
+        }
+        const int64_t rr0 = (int64_t)((f.s - 4) >> 7) - (int64_t)r0;
+        const int64_t rr1 = (int64_t)((f.s - 1) >> 7) - (int64_t)r0;
+        const int64_t rre = f.e > f.s ? (int64_t)((f.e - 1) >> 7) - (int64_t)r0 : -1;
+        rs0 = rr0 >= 0 && rr0 < rows ? (uint32_t)rr0 : ~0u;
+        rs1 = rr1 >= 0 && rr1 < rows ? (uint32_t)rr1 : ~0u;
+        re = rre >= 0 && rre < rows ? (uint32_t)rre : ~0u;
+      }
       if (r0 * kRowBytes < f.s) {  // the init bytes [s-4, s) may straddle two units
         const uint32_t v = (args.init ? args.init[b] : 0u) ^ 0xffffffffu;
         u = nib_glb(dc->neg4_nib, v);
@@ -324,34 +366,29 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 32));
     rows_max = __builtin_amdgcn_readfirstlane(rows_max);
 
-    // A safe load address for every lane and row: rows past this unit, idle
-    // lanes and edge chunks wholly outside [s, e) read the zero pad instead.
-    // Branch-free on purpose (bitwise & |): with short-circuit && / || the
-    // structurizer turned the select below into control flow and lost the
-    // pad address for lanes whose value is dead -- they then loaded from
-    // their raw row address (observed: reads below the batch, a GPU fault).
-    auto row_ok = [&](uint32_t r) -> bool {
-      const uint64_t a = row_a + (uint64_t)r * kRowBytes;
-      const bool inside = (a + 16 > f.s) & (a < f.e) & (f.s < f.e);
-      return (r < rows) & ((!edge) | inside);
-    };
+    // Row r of this lane is loaded from its address when r in [r_lo, r_hi),
+    // else from the zero pad.  Branch-free select, and the address pinned in
+    // every lane: where a lane's value is dead, hipcc otherwise left that
+    // lane's address undefined although the wave still issues the load
+    // (observed: reads below the batch, a GPU fault).
     auto row_addr = [&](uint32_t r) -> gptr_u32x4 {
-      uint64_t p = row_ok(r) ? row_a + (uint64_t)r * kRowBytes : dummy;
-      asm volatile("" : "+v"(p));  // materialise the per-lane address before the load
+      const bool ok = (r >= r_lo) & (r < r_hi);
+      uint64_t p = ok ? row_a + (uint64_t)r * kRowBytes : dummy;
 #ifdef LSBM_DEBUG_BOUNDS  // diagnostic builds only: report and neutralise wild loads
       if (p != dummy && (p + 16 <= args.dbg_lo || p >= args.dbg_hi)) {
-        printf("OOB wave %lu lane %u b %lu o %u r %u rows %u edge %d s %lx e %lx row_a %lx p %lx\n",
-               (unsigned long)wave, lane, (unsigned long)b, o, r, rows, (int)edge,
-               (unsigned long)f.s, (unsigned long)f.e, (unsigned long)row_a, (unsigned long)p);
+        printf("OOB wave %lu lane %u b %lu o %u r %u rows %u s %lx e %lx row_a %lx p %lx\n",
+               (unsigned long)wave, lane, (unsigned long)b, o, r, rows, (unsigned long)f.s,
+               (unsigned long)f.e, (unsigned long)row_a, (unsigned long)p);
         p = dummy;
       }
 #endif
+      asm volatile("" : "+v"(p));
       return reinterpret_cast<gptr_u32x4>(p);
     };
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
     auto absorb = [&](u32x4 w, uint32_t r) {  // rows read from the pad are zero
-      const uint64_t a = row_a + (uint64_t)r * kRowBytes;
-      if (edge && (a < f.s || a + 16 > f.e)) {
+      if ((r == rs0) | (r == rs1) | (r == re)) {
+        const uint64_t a = row_a + (uint64_t)r * kRowBytes;
         w.x = frame_word(w.x, a, f.s, f.e, u);
         w.y = frame_word(w.y, a + 4, f.s, f.e, u);
         w.z = frame_word(w.z, a + 8, f.s, f.e, u);
@@ -386,14 +423,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
 #endif
       if (li == 0) atomicXor(args.acc + b, contrib);
     }
-    // advance the cursor by 8 units (uniform: every lane walks the same path)
-    cur_o += 8;
-    while (cur_b < b_hi) {
-      const uint32_t m = block_frame(args, cur_b).units;
-      if (cur_o < m) break;
-      cur_o -= m;
-      cur_b++;
-    }
+    // advance the cursor past the 8 units just taken
+    const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
+    const uint32_t pre8 = jnext ? pre8_prev : 0u;
+    cur_b += jnext;
+    cur_o = cur_o + 8 - pre8;
   }
 }
 
