@@ -73,6 +73,14 @@ int lsbm_crc32c_fixed_dev(const void* d_base, uint64_t stride, uint64_t len, uin
 int lsbm_crc32c_batch_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks,
                           const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
 
+/* Extent-list batch: block i = d_base[ext[2i], ext[2i] + ext[2i+1]) ({offset,
+ * length} pairs, any order, may overlap).  For records that are not
+ * contiguous, e.g. WAL payloads between their 7-byte headers: with
+ * d_init[i] = type_crc_[t] and LSBM_CRC32C_MASKED this is exactly
+ * log::Writer::EmitPhysicalRecord's header CRC (common/log_writer.cc:86-87). */
+int lsbm_crc32c_extents_dev(const void* d_base, const uint64_t* d_extents, uint64_t n_blocks,
+                            const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
+
 /* Ragged verify: d_ok[i] = (crc of block i == d_expect[i]) where d_expect holds
  * masked values if flags has LSBM_CRC32C_MASKED.  If d_nbad != NULL the
  * number of mismatches is ADDED to *d_nbad (caller zeroes it). */

@@ -35,6 +35,7 @@ SIGNATURES = {
     "lsbm_crc32c_last_error": (ctypes.c_char_p, []),
     "lsbm_crc32c_fixed_dev": (_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u32, _vp]),
     "lsbm_crc32c_batch_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _u32, _vp]),
+    "lsbm_crc32c_extents_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _u32, _vp]),
     "lsbm_crc32c_verify_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp]),
     "lsbm_sst_seal_dev": (_int, [_vp, _vp, _vp, _u64, _vp]),
     "lsbm_sst_verify_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp]),

@@ -348,6 +348,24 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_dev(
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
+__attribute__((visibility("default"))) int lsbm_crc32c_extents_dev(
+    const void* d_base, const uint64_t* d_extents, uint64_t n_blocks, const uint32_t* d_init,
+    uint32_t* d_out, uint32_t flags, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_base || !d_extents || !d_out) return fail(LSBM_ERR_INVALID, "null pointer");
+  if (flags & ~LSBM_CRC32C_MASKED) return fail(LSBM_ERR_INVALID, "unknown flags");
+  RaggedArgs a = {};
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.handles = d_extents;  // {offset, size} pairs, the BlockHandle layout
+  a.extents = kExtHandles;
+  a.n = n_blocks;
+  a.init = d_init;
+  a.out = d_out;
+  a.flags = flags;
+  a.mode = kModeOut;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
 __attribute__((visibility("default"))) int lsbm_crc32c_verify_dev(
     const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks, const uint32_t* d_init,
     const uint32_t* d_expect, uint8_t* d_ok, uint32_t* d_nbad, uint32_t flags, void* stream) {

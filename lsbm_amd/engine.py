@@ -6,6 +6,7 @@ and returns without synchronising.  Nothing here computes on the CPU.
 
   crc32c_fixed(data, stride, length, n_blocks)   lsbm_crc32c_fixed_dev
   crc32c_batch(data, offsets)                    lsbm_crc32c_batch_dev
+  crc32c_extents(data, extents)                  lsbm_crc32c_extents_dev
   crc32c_verify(data, offsets, expect)           lsbm_crc32c_verify_dev
   crc32c_batch_host(data_np, offsets_np)         lsbm_crc32c_batch_host
   fill_splitmix64(buf, seed), stream_read(buf)   benchmark helpers
@@ -81,6 +82,22 @@ def crc32c_batch(data, offsets, init=None, masked=False, out=None, stream=None):
     check(lib().lsbm_crc32c_batch_dev(_ptr(data), _ptr(offsets), max(n, 0), _ptr(init),
                                       _ptr(out), flags, _stream_ptr(stream)),
           "lsbm_crc32c_batch_dev")
+    return out
+
+
+def crc32c_extents(data, extents, init=None, masked=False, out=None, stream=None):
+    """Block i = data[ext[2i] : ext[2i] + ext[2i+1]] (int64 {offset, length} pairs)."""
+    torch = _torch()
+    _require_cuda(data, extents, init, out)
+    if extents.dtype != torch.int64 or extents.numel() % 2:
+        raise ValueError("extents must be int64 {offset, length} pairs")
+    n = extents.numel() // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    flags = LSBM_CRC32C_MASKED if masked else 0
+    check(lib().lsbm_crc32c_extents_dev(_ptr(data), _ptr(extents), n, _ptr(init), _ptr(out),
+                                        flags, _stream_ptr(stream)),
+          "lsbm_crc32c_extents_dev")
     return out
 
 
