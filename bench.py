@@ -155,9 +155,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # LSBM_BENCH_DEVICES lets a rehearsal put several ranks on fewer GPUs;
+    # LSBM_BENCH_BACKEND=gloo rehearses the multi-rank flow without RCCL.
+    ndev = int(os.environ.get("LSBM_BENCH_DEVICES", "0")) or torch.cuda.device_count()
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("LSBM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from lsbm_amd import engine
     engine.init(local)
@@ -177,7 +185,8 @@ def main():
             dist.barrier()
 
     def max_reduce(x):
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        on_gpu = os.environ.get("LSBM_BENCH_BACKEND", "nccl") == "nccl"
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())

@@ -284,3 +284,29 @@ def test_host_staged_pinned_source_and_chunking(torch_cuda, oracle):
     got = engine.crc32c_batch_host(view, offs, masked=True)
     want = oracle.batch_offsets(view, offs, masked=True)
     assert np.array_equal(got, want)
+
+
+def test_fixed_batch_replays_in_a_hip_graph(torch_cuda, oracle):
+    """lsbm_crc32c_fixed_dev only enqueues (no alloc / sync), so it can be
+    captured into a graph (torch.cuda.CUDAGraph = hipGraph) and replayed."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n, L = 4096, 4096
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 0xABC)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        engine.crc32c_fixed(d, L, L, n, out=out, stream=torch.cuda.current_stream())
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    want = oracle.batch_fixed(stream_bytes(0xABC, 0, n * L), L, L, n)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    engine.fill_splitmix64(d, 0xABD)  # new bytes, same graph
+    g.replay()
+    torch.cuda.synchronize()
+    want2 = oracle.batch_fixed(stream_bytes(0xABD, 0, n * L), L, L, n)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want2)
