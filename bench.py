@@ -10,15 +10,18 @@ of every block, util/crc32c.cc:286-329).
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 With N > 1 it is launched by torch.distributed.run, one process per GPU; each
-rank checksums its own 1M-block shard (weak scaling, no data-path collective:
-blocks are independent).  Timing: W untimed steps, barrier + synchronize, K
+rank checksums its own shard of 10M x 4 KiB blocks (BASELINE.json configs[4]:
+80M blocks over 8 GPUs; weak scaling, no data-path collective: blocks are
+independent).  --blocks overrides the per-GPU block count.  Timing: W untimed steps, barrier + synchronize, K
 steps between HIP events on the launch stream, barrier + synchronize, max over
 ranks.  Rank 0 prints ONE JSON line.
 
 Extra fields: roofline (achieved algorithmic GB/s of the dominant kernel vs the
 8 TB/s HBM peak), cpu_baseline (the reference CPU CRC on the host cores, rank 0
 at N=1 only, bounded sample), stream_read (the same buffer read with the CRC
-kernel's own access pattern and no CRC work: the measured read ceiling).
+kernel's own access pattern and no CRC work: the measured read ceiling),
+host_staged (the same blocks checksummed from pinned host memory through
+lsbm_crc32c_batch_host: the PCIe-inclusive rate, rank 0 at N=1 only).
 """
 import argparse
 import ctypes
@@ -35,7 +38,8 @@ sys.path.insert(0, REPO)
 METRIC = "CRC32C GiB/s over device-resident 4 KiB SSTable blocks (1 GPU); % HBM peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X spec, MI355X_MICROARCH.md "Chip-level parameters"
 BLOCK = 4096
-NBLOCKS = 1 << 20
+NBLOCKS = 1 << 20            # configs[1]: 1M x 4 KiB on one GPU
+NBLOCKS_MULTI = 10_000_000   # configs[4]: 80M x 4 KiB over 8 GPUs = 10M per GPU
 SEED = 0x5EED0000
 
 
@@ -44,7 +48,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--blocks", type=int, default=NBLOCKS, help=argparse.SUPPRESS)
+    p.add_argument("--blocks", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="aggregate CPU-seconds for the cpu_baseline sample")
@@ -129,6 +133,14 @@ def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
         if el * threads >= cpu_seconds or el > 30:
             break
     gib = passes * sample_blocks * BLOCK / 2**30
+    # one core, bounded to ~3 s (1 thread and all threads)
+    p1, t1 = 0, time.perf_counter()
+    while True:
+        f(data.ctypes.data, BLOCK, BLOCK, 8192, out.ctypes.data, 1)
+        p1 += 1
+        el1 = time.perf_counter() - t1
+        if el1 >= 3.0:
+            break
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -142,7 +154,31 @@ def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
             "sample": f"{passes} passes x {sample_blocks} x {BLOCK} B blocks (first blocks of "
                       f"the rank-0 buffer, host copy), crc32c::Value slice-by-4, "
                       f"{threads} pthreads, {el:.1f} s wall; {cpu_model}",
+            "single_thread": {"value": round(p1 * 8192 * BLOCK / 2**30 / el1, 3), "unit": "GiB/s",
+                              "cores": 1, "sample": f"{p1} passes x 8192 blocks, {el1:.1f} s"},
             "gpu_mismatches_on_sample": mismatches}
+
+
+def host_staged(engine, data, gpu_crcs, n_blocks, reps=3):
+    """PCIe-inclusive rate: blocks start in PINNED host memory,
+    lsbm_crc32c_batch_host DMAs them to the GPU (hipMemcpyAsync, 64 MiB chunks
+    over 3 streams overlapped with the kernel) and returns 4 B/block to the
+    host.  Never the headline `value`: the north_star metric is device-resident."""
+    import torch
+    src = torch.empty(n_blocks * BLOCK, dtype=torch.uint8, pin_memory=True)
+    src.copy_(data[:n_blocks * BLOCK])
+    h = src.numpy()
+    offs = np.arange(0, (n_blocks + 1) * BLOCK, BLOCK, dtype=np.uint64)
+    engine.crc32c_batch_host(h[:BLOCK * 1024], offs[:1025])  # staging buffers
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = engine.crc32c_batch_host(h, offs)
+    el = (time.perf_counter() - t0) / reps
+    return {"GBps": round(n_blocks * BLOCK / el / 1e9, 2),
+            "GiBps": round(n_blocks * BLOCK / el / 2**30, 2),
+            "sample": f"{n_blocks} x {BLOCK} B blocks from pinned host memory, {reps} passes, "
+                      "host->device DMA + kernel + 4 B/block back, wall clock",
+            "mismatches_vs_device_path": int(np.count_nonzero(got != gpu_crcs[:n_blocks]))}
 
 
 def main():
@@ -169,7 +205,7 @@ def main():
 
     from lsbm_amd import engine
     engine.init(local)
-    n = args.blocks
+    n = args.blocks or (NBLOCKS if world == 1 else NBLOCKS_MULTI)
     data = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
     engine.fill_splitmix64(data, SEED + rank)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -214,9 +250,10 @@ def main():
     workload = f"{n} x {BLOCK} B device-resident blocks per GPU, batched crc32c::Value"
     traffic = load_traffic(workload)
 
-    cpu = None
+    cpu = staged = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gpu_crcs = out.cpu().numpy().view(np.uint32)
+        staged = host_staged(engine, data, gpu_crcs, min(n, 1 << 18))
         cpu = cpu_baseline(min(n, 65536), gpu_crcs, args.cpu_seconds)
 
     if rank == 0:
@@ -235,7 +272,10 @@ def main():
             "data": f"synthetic: on-device splitmix64 bytes (seed 0x{SEED:X} + rank), "
                     "resident in HBM before timing",
             "config": {"workload": workload, "blocks_per_gpu": n, "block_bytes": BLOCK,
-                       "stride": BLOCK, "baseline_config": "BASELINE.json configs[1]",
+                       "stride": BLOCK,
+                       "baseline_config": "BASELINE.json configs[1]" if n == NBLOCKS and world == 1
+                       else ("BASELINE.json configs[4] (10M x 4 KiB per GPU, weak scaling)"
+                             if n == NBLOCKS_MULTI else "custom"),
                        "parallelism": f"{world} independent shards, no collective"},
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBPS, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -247,6 +287,7 @@ def main():
             "stream_read": {"GBps": round(stream_gbps, 1),
                             "crc_frac_of_stream_read": round(achieved / stream_gbps, 4)},
             "cpu_baseline": cpu,
+            "host_staged": staged,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -19,3 +19,4 @@ for grp in "FETCH_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC
   [ $rc -eq 0 ] || exit $rc
 done
 python3 tools/traffic.py $OUT && cp profiles/traffic.json $OUT/
+grep "^{\"metric" $OUT/stats.log > $OUT/stats_bench_line.json
