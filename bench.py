@@ -174,7 +174,17 @@ def host_staged(engine, data, gpu_crcs, n_blocks, reps=3):
     for _ in range(reps):
         got = engine.crc32c_batch_host(h, offs)
     el = (time.perf_counter() - t0) / reps
+    # the PCIe ceiling: a plain pinned H2D copy of the same bytes
+    dst = torch.empty_like(src, device="cuda")
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    el_copy = (time.perf_counter() - t0) / reps
     return {"GBps": round(n_blocks * BLOCK / el / 1e9, 2),
+            "h2d_copy_GBps": round(n_blocks * BLOCK / el_copy / 1e9, 2),
             "GiBps": round(n_blocks * BLOCK / el / 2**30, 2),
             "sample": f"{n_blocks} x {BLOCK} B blocks from pinned host memory, {reps} passes, "
                       "host->device DMA + kernel + 4 B/block back, wall clock",

@@ -10,6 +10,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsbm_crc32c.so")
+# diagnostic builds (tools/ablate_units.sh) are loaded through LSBM_LIB_PATH
+LIB_PATH = os.environ.get("LSBM_LIB_PATH") or LIB_PATH
 
 # status codes (include/lsbm_crc32c.h)
 LSBM_OK = 0

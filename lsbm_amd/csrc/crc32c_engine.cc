@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -83,6 +84,7 @@ void build_consts(DevConsts* c) {
   }
   for (uint32_t i = 0; i < 16; i++)  // A^(4096 * 2^i) = A^(2^(12+i))
     memcpy(&c->lds_image[kNibU4096 / 4 + i * 128], c->pow_nib[12 + i], 512);
+  memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
   memset(c->zero16, 0, sizeof(c->zero16));
 }
 
@@ -464,8 +466,13 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
   std::lock_guard<std::mutex> lock(stg.mu);
   const uint8_t* src = static_cast<const uint8_t*>(h_base);
   const bool src_pinned = host_pinned(h_base);
-  constexpr uint64_t kChunkBytes = 64ull << 20;
-  constexpr uint64_t kChunkBlocks = 1ull << 16;
+  // chunk size: LSBM_STAGE_CHUNK_MB overrides (tuning only; tools/host_sweep.py)
+  static const uint64_t kChunkBytes = [] {
+    const char* v = getenv("LSBM_STAGE_CHUNK_MB");
+    const long mb = v ? atol(v) : 0;
+    return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 64) << 20;
+  }();
+  const uint64_t kChunkBlocks = kChunkBytes >> 10;
   const int nslots = 3;
   int si = 0;
   uint64_t next = 0;

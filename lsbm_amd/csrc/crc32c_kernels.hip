@@ -195,35 +195,60 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 // A^(4096 k), is xor-ed into acc[block]; the finish kernel turns acc into
 // the CRC and applies the output mode.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t frame_word(uint32_t raw, uint64_t a, uint64_t s, uint64_t e,
-                                               uint32_t u) {
-  // keep the bytes of the dword at address a that lie in [s, e)
-  const int64_t lo = (int64_t)s - (int64_t)a, hi = (int64_t)e - (int64_t)a;
-  const uint32_t l = lo < 0 ? 0u : (lo > 4 ? 4u : (uint32_t)lo);
-  const uint32_t h = hi < 0 ? 0u : (hi > 4 ? 4u : (uint32_t)hi);
-  const uint64_t keep = h > l ? (((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull)) : 0ull;
-  uint32_t w = raw & (uint32_t)keep;
-  // virtual init bytes u at [s-4, s)
-  const int64_t d = (int64_t)a - ((int64_t)s - 4);
-  if (d >= 0 && d < 4) w ^= u >> (8 * d);
-  else if (d < 0 && d > -4) w ^= u << (8 * (-d));
-  return w;
+// Byte n of a little-endian word and below: (1 << 8n) - 1, n in [0, 4].
+__device__ __forceinline__ uint32_t low_bytes(int32_t n) {
+  return (uint32_t)((1ull << (8 * n)) - 1ull);
+}
+
+// The word at byte p of a 16-B chunk, fixed for the frame: keep the bytes in
+// [ds, de) (s and e relative to the chunk) and add the virtual init bytes u
+// at [ds - 4, ds).
+__device__ __forceinline__ uint32_t fix_word(uint32_t w, int32_t ds, int32_t de, uint32_t u,
+                                             int32_t p) {
+  const int32_t lo = min(max(ds - p, 0), 4), hi = min(max(de - p, 0), 4);
+  const uint32_t keep = low_bytes(hi) & ~low_bytes(lo);
+  const int32_t d = p + 4 - ds;  // the word's offset from s - 4
+  uint32_t inj = 0;
+  if (d >= 0 && d < 4) inj = u >> (8 * d);
+  else if (d < 0 && d > -4) inj = u << (-8 * d);
+  return (w & keep) ^ inj;
+}
+
+// The two 64-bit words that define block b's extent (offsets[b], offsets[b+1]
+// or a BlockHandle {offset, size}); nothing is loaded for fixed extents.
+struct ExtRaw {
+  uint64_t x, y;
+};
+typedef const __attribute__((address_space(1))) uint64_t* gptr_u64;
+typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;
+
+__device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) {
+  ExtRaw r = {0, 0};
+  if (a.extents == kExtHandles) {
+    const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
+    r.x = h[2 * b];
+    r.y = h[2 * b + 1];
+  } else if (a.extents == kExtOffsets) {
+    const gptr_u64 o = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.offsets));
+    r.x = o[b];
+    r.y = o[b + 1];
+  }
+  return r;
 }
 
 // Block b's extent [s, e) as absolute addresses.
-__device__ __forceinline__ void block_extent(const RaggedArgs& a, uint64_t b, uint64_t& s,
-                                             uint64_t& e) {
+__device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b, ExtRaw r,
+                                                uint64_t& s, uint64_t& e) {
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
   if (a.extents == kExtHandles) {
-    const uint64_t off = a.handles[2 * b], sz = a.handles[2 * b + 1];
-    s = base + off;
-    e = s + sz + (a.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
+    s = base + r.x;
+    e = s + r.y + (a.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
   } else if (a.extents == kExtFixed) {
     s = base + b * a.stride;
     e = s + a.len;
   } else {
-    s = base + a.offsets[b];
-    e = base + a.offsets[b + 1];
+    s = base + r.x;
+    e = base + r.y;
     if (e < s) e = s;
   }
 }
@@ -233,14 +258,21 @@ struct Frame {
   uint32_t units;             // ceil(rows / 32)
 };
 
-__device__ __forceinline__ Frame block_frame(const RaggedArgs& a, uint64_t b) {
+__device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e) {
   Frame f;
-  block_extent(a, b, f.s, f.e);
-  f.row0 = (f.s - 4) >> 7;
-  const uint64_t row_end = (f.e + 127) >> 7;
+  f.s = s;
+  f.e = e;
+  f.row0 = (s - 4) >> 7;
+  const uint64_t row_end = (e + 127) >> 7;
   f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
   f.units = (uint32_t)((f.rows + kUnitRows - 1) / kUnitRows);
   return f;
+}
+
+__device__ __forceinline__ Frame block_frame(const RaggedArgs& a, uint64_t b) {
+  uint64_t s, e;
+  extent_from_raw(a, b, load_ext_raw(a, b), s, e);
+  return frame_of(s, e);
 }
 
 // M(v) for nibble tables in LDS at byte offset `tab` (low 6 bits clear).
@@ -262,9 +294,14 @@ __device__ __forceinline__ uint32_t shift_units(const uint32_t* lds, const DevCo
   return v;
 }
 
+// Units kernel.  Each wave owns a contiguous range of blocks and walks it in
+// rounds of 8 units (one per lane group).  The loop is software-pipelined so
+// that no global-memory latency is exposed between rounds:
+//   * the extents of the next round's blocks are loaded one round ahead;
+//   * a round issues its first bank of row loads, THEN merges the previous
+//     round's braids (LDS work overlapping the loads), then streams its rows.
 __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
   const DevConsts* __restrict__ dc = args.dc;
-  load_lds_tables(g_lds, dc);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
   const uint32_t lb = (lane & 31u) << 2;
@@ -276,24 +313,62 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   // this wave's contiguous range of blocks
   const uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
+  const uint32_t* __restrict__ init = args.init;
+  const uint32_t jl = lane < 8u ? lane : 8u;  // lanes 0..8 hold the walk's 9 blocks
 #ifdef LSBM_DEBUG_BOUNDS
   if (threadIdx.x == 0 && blockIdx.x == 0)
     printf("units: n %lu base %lx dbg [%lx, %lx) acc %p dc %p dummy %lx grid %u\n", (unsigned long)args.n,
            (unsigned long)args.base, (unsigned long)args.dbg_lo, (unsigned long)args.dbg_hi, args.acc, dc,
            (unsigned long)dummy, gridDim.x);
 #endif
+  // extents (+ init) of blocks nb + jl, clamped into the range so that the
+  // loads are unconditional; only lanes with nb + lane < b_hi use them
+  auto prefetch = [&](uint64_t nb, ExtRaw& r, uint32_t& iv) {
+    uint64_t idx = nb + jl;
+    idx = idx < b_hi ? idx : b_hi - 1;
+    r = load_ext_raw(args, idx);
+    iv = init ? reinterpret_cast<gptr_u32>(reinterpret_cast<uint64_t>(init))[idx] : 0u;
+  };
 
   // wave cursor: unit ordinal `cur_o` of block `cur_b` is the next unassigned unit
   uint64_t cur_b = b_lo;
   uint32_t cur_o = 0;
+  ExtRaw rj = {0, 0};
+  uint32_t ivj = 0;
+  if (b_lo < b_hi) prefetch(cur_b, rj, ivj);
+  load_lds_tables(g_lds, dc);  // overlaps the first extents' latency
+
+  // the previous round's braids and destination
+  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, pk = 0;
+  uint64_t pb = 0;
+  bool pact = false;
+  auto retire = [&]() {  // merge the previous round's braids into acc
+#if defined(LSBM_ABL_U_NOMERGE)  // diagnostic builds only (wrong CRCs)
+    const uint32_t raw = p0;
+#else
+    const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
+#endif
+    if (pact) {
+      const uint32_t contrib = shift_units(g_lds, dc, raw, pk);
+#ifdef LSBM_DEBUG_BOUNDS
+      if (li == 0 && pb >= args.n) printf("ACC OOB wave %lu b %lu n %lu\n", (unsigned long)wave, (unsigned long)pb, (unsigned long)args.n);
+      else
+#endif
+      if (li == 0) atomicXor(args.acc + pb, contrib);
+    }
+  };
+
   while (cur_b < b_hi) {
-    // Find the 8 groups' units in one round: lane j reads block cur_b + j
+    // Find the 8 groups' units in one round: lane j holds block cur_b + j
     // (8 units never span more than 9 blocks), an inclusive prefix sum over
-    // the lanes' unit counts, then one ballot per group.
-    const uint64_t bj = cur_b + lane;
-    Frame fj = {0, 0, 0, 1, 0};
-    if (lane < 9 && bj < b_hi) fj = block_frame(args, bj);
-    uint32_t pre = fj.units;
+    // the lanes' unit counts, then one ballot per group.  ALU + shuffles only:
+    // the extents arrived during the previous round.
+    uint64_t sj = 0, ej = 0;
+    extent_from_raw(args, cur_b + lane, rj, sj, ej);
+    const Frame ft = frame_of(sj, ej);
+    const bool vj = lane < 9u && cur_b + lane < b_hi;
+    const uint32_t units_j = vj ? ft.units : 0u;
+    uint32_t pre = units_j;
 #pragma unroll
     for (uint32_t d = 1; d < 16; d <<= 1) {  // lanes >= 9 contribute 0: a 16-lane scan suffices
       const uint32_t t = (uint32_t)__shfl_up((int)pre, d, 16);
@@ -316,23 +391,36 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint64_t b = cur_b + jg;
     const bool active = jg < 9 && b < b_hi;
     Frame f = {0, 0, 0, 1, 1};
-    f.s = __shfl((unsigned long long)fj.s, (int)jg);
-    f.e = __shfl((unsigned long long)fj.e, (int)jg);
-    f.row0 = __shfl((unsigned long long)fj.row0, (int)jg);
-    f.rows = __shfl((unsigned long long)fj.rows, (int)jg);
-    f.units = (uint32_t)__shfl((int)fj.units, (int)jg);
+    f.s = __shfl((unsigned long long)ft.s, (int)jg);
+    f.e = __shfl((unsigned long long)ft.e, (int)jg);
+    f.row0 = __shfl((unsigned long long)ft.row0, (int)jg);
+    f.rows = __shfl((unsigned long long)ft.rows, (int)jg);
+    f.units = (uint32_t)__shfl((int)ft.units, (int)jg);
+    const uint32_t iv = (uint32_t)__shfl((int)ivj, (int)jg);
     const uint32_t o = my_t - pre_before;
+    // the cursor after these 8 units, and the next round's extents
+    const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
+    const uint32_t pre8 = jnext ? pre8_prev : 0u;
+    const uint64_t nb = cur_b + jnext;
+    const uint32_t no = cur_o + 8 - pre8;
+    ExtRaw rn;
+    uint32_t ivn;
+    prefetch(nb, rn, ivn);
 
     uint32_t rows = 0, k = 0;
     uint64_t row_a = dummy;  // absolute address of this lane's slice of the unit's first row
-    // rows whose loads are inside [s, e): [r_lo, r_hi); rows needing the
-    // masking / init-byte fix: rs0, rs1 (around s) and re (holding e - 1)
-    uint32_t r_lo = 0, r_hi = 0, rs0 = ~0u, rs1 = ~0u, re = ~0u;
-    uint32_t u = 0;
+    uint64_t r0 = 0;
+    // rows whose loads are inside [s, e): [r_lo, r_hi).  Per lane at most two
+    // rows need a fix (fix_word): rfs, whose chunk starts before s and holds
+    // init bytes of [s-4, s) or straddles s (s - chunk in [1, 19]), and rfe,
+    // whose chunk straddles e (e - chunk in [1, 15]).  ds / de: s / e relative
+    // to the chunk (-64 / 64: no cut).
+    uint32_t r_lo = 0, r_hi = 0, rfs = ~0u, rfe = ~0u;
+    int32_t ds = -64, de_s = 64, de_e = 64;
     if (active) {
       const uint32_t first_rows = (uint32_t)(f.rows - (uint64_t)kUnitRows * (f.units - 1));
       rows = o == 0 ? first_rows : kUnitRows;
-      const uint64_t r0 = f.row0 + (o == 0 ? 0 : first_rows + (uint64_t)kUnitRows * (o - 1));
+      r0 = f.row0 + (o == 0 ? 0 : first_rows + (uint64_t)kUnitRows * (o - 1));
       row_a = r0 * kRowBytes + 16u * li;
       k = f.units - 1 - o;
       const bool edge = r0 * kRowBytes < f.s || (r0 + rows) * kRowBytes > f.e;
@@ -347,16 +435,22 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
           r_lo = (uint32_t)(lo < (int64_t)rows ? lo : rows);
           r_hi = (uint32_t)(hi < (int64_t)rows ? hi : rows);
         }
-        const int64_t rr0 = (int64_t)((f.s - 4) >> 7) - (int64_t)r0;
-        const int64_t rr1 = (int64_t)((f.s - 1) >> 7) - (int64_t)r0;
-        const int64_t rre = f.e > f.s ? (int64_t)((f.e - 1) >> 7) - (int64_t)r0 : -1;
-        rs0 = rr0 >= 0 && rr0 < rows ? (uint32_t)rr0 : ~0u;
-        rs1 = rr1 >= 0 && rr1 < rows ? (uint32_t)rr1 : ~0u;
-        re = rre >= 0 && rre < rows ? (uint32_t)rre : ~0u;
-      }
-      if (r0 * kRowBytes < f.s) {  // the init bytes [s-4, s) may straddle two units
-        const uint32_t v = (args.init ? args.init[b] : 0u) ^ 0xffffffffu;
-        u = nib_glb(dc->neg4_nib, v);
+        const int64_t t_s = (int64_t)f.s - 1 - (int64_t)row_a;
+        if (t_s >= 0 && (t_s & 127) < 19 && (t_s >> 7) < (int64_t)rows) {
+          rfs = (uint32_t)(t_s >> 7);
+#ifdef LSBM_DEBUG_BOUNDS
+          if (rfs > 1) printf("RFS %u b %lu o %u\n", rfs, (unsigned long)b, o);
+#endif
+          ds = (int32_t)(t_s & 127) + 1;
+          const int64_t ee = (int64_t)f.e - (int64_t)(row_a + (uint64_t)rfs * kRowBytes);
+          de_s = ee < 64 ? (int32_t)ee : 64;
+        }
+        const int64_t t_e = (int64_t)f.e - 1 - (int64_t)row_a;
+        if (t_e >= 0 && (t_e & 127) < 15 && (t_e >> 7) < (int64_t)rows &&
+            (uint32_t)(t_e >> 7) != rfs) {
+          rfe = (uint32_t)(t_e >> 7);
+          de_e = (int32_t)(t_e & 127) + 1;
+        }
       }
     }
     // uniform trip count: the longest unit of the 8 groups
@@ -385,50 +479,105 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       asm volatile("" : "+v"(p));
       return reinterpret_cast<gptr_u32x4>(p);
     };
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    auto absorb = [&](u32x4 w, uint32_t r) {  // rows read from the pad are zero
-      if ((r == rs0) | (r == rs1) | (r == re)) {
-        const uint64_t a = row_a + (uint64_t)r * kRowBytes;
-        w.x = frame_word(w.x, a, f.s, f.e, u);
-        w.y = frame_word(w.y, a + 4, f.s, f.e, u);
-        w.z = frame_word(w.z, a + 8, f.s, f.e, u);
-        w.w = frame_word(w.w, a + 12, f.s, f.e, u);
-      }
-      if (r < rows) STEP_ROW(w);
-    };
     // two banks of 4 rows, loads always issued (pad reads past the unit) so
     // that the loads in flight are counted exactly
     u32x4 ba[4], bb[4];
 #pragma unroll
     for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(k2));
-    for (uint32_t r = 0; r < rows_max; r += 8) {
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 4; k2++) bb[k2] = __builtin_nontemporal_load(row_addr(r + 4 + k2));
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(ba[k2], r + k2);
-      if (r + 4 >= rows_max) break;
-      if (r + 8 < rows_max) {
-#pragma unroll
-        for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(r + 8 + k2));
+    // the chunk straddling e sits in the unit's last row (rfe = rows - 1): its
+    // bytes >= e are removed after the loop (below), from this early copy
+    uint64_t pe = rfe != ~0u ? row_a + (uint64_t)rfe * kRowBytes : dummy;
+    asm volatile("" : "+v"(pe));
+    const u32x4 wl = *reinterpret_cast<gptr_u32x4>(pe);
+
+    // while those loads fly: the init bytes and the previous round's merge
+    const uint32_t u = nib_lds_at(g_lds, kNibNeg4, iv ^ 0xffffffffu);  // A^-4(init ^ ~0)
+    retire();
+
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    auto absorb = [&](u32x4 w, uint32_t r) {  // rows read from the pad are zero
+      // Consume the loaded row in straight-line code: with the only use inside
+      // the (r < rows) branch, the vmcnt wait sat on that path alone, and the
+      // next reload of the bank had to drain every load still in flight.
+      asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+      if (r < rows) STEP_ROW(w);
+    };
+    // The start fix (init bytes, bytes before s) only ever falls on rows 0
+    // and 1 of a unit: chunk c of row 0 has c <= s - 4 and the fix chunk has
+    // c >= s - 19.
+    auto absorb_start = [&](u32x4 w, uint32_t r) {
+#ifndef LSBM_ABL_U_NOFIX  // diagnostic builds only: skip the edge masking (wrong CRCs)
+      if (rfs == r) {
+        w.x = fix_word(w.x, ds, de_s, u, 0);
+        w.y = fix_word(w.y, ds, de_s, u, 4);
+        w.z = fix_word(w.z, ds, de_s, u, 8);
+        w.w = fix_word(w.w, ds, de_s, u, 12);
       }
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(bb[k2], r + 4 + k2);
-    }
-    const uint32_t raw = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
-    if (active) {
-      const uint32_t contrib = shift_units(g_lds, dc, raw, k);
-#ifdef LSBM_DEBUG_BOUNDS
-      if (li == 0 && b >= args.n) printf("ACC OOB wave %lu b %lu n %lu\n", (unsigned long)wave, (unsigned long)b, (unsigned long)args.n);
-      else
 #endif
-      if (li == 0) atomicXor(args.acc + b, contrib);
+      absorb(w, r);
+    };
+    // Every bank load is unconditional (rows past the unit read the pad): with
+    // a load skipped on one path, the vmcnt waits after the merge point must
+    // assume the shorter queue and over-wait on the other path.
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < 4; k2++) bb[k2] = __builtin_nontemporal_load(row_addr(4 + k2));
+    absorb_start(ba[0], 0);
+    absorb_start(ba[1], 1);
+    absorb(ba[2], 2);
+    absorb(ba[3], 3);
+    // End fix.  The register kept per braid is the pre-lookup word c = s ^ w
+    // of the last row absorbed, so dropping the bytes >= e of that row is a
+    // plain xor after the loop: c ^= w & ~keep (lanes without rfe: de_e = 64,
+    // keep = ~0).  Computed here, pinned, so that no wait follows the loop.
+    uint32_t dx = wl.x & ~low_bytes(min(max(de_e, 0), 4));
+    uint32_t dy = wl.y & ~low_bytes(min(max(de_e - 4, 0), 4));
+    uint32_t dz = wl.z & ~low_bytes(min(max(de_e - 8, 0), 4));
+    uint32_t dw = wl.w & ~low_bytes(min(max(de_e - 12, 0), 4));
+    asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(dw));
+    // fully unrolled (rows_max <= kUnitRows): a rolled loop got a vmcnt(0) at
+    // its header, draining the bank in flight every 8 rows
+#pragma unroll
+    for (uint32_t r = 4; r < kUnitRows; r += 8) {
+      if (r >= rows_max) break;
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(r + 4 + k2));
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(bb[k2], r + k2);
+      if (r + 4 >= rows_max) break;
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) bb[k2] = __builtin_nontemporal_load(row_addr(r + 8 + k2));
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 4; k2++) absorb(ba[k2], r + 4 + k2);
     }
-    // advance the cursor past the 8 units just taken
-    const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
-    const uint32_t pre8 = jnext ? pre8_prev : 0u;
-    cur_b += jnext;
-    cur_o = cur_o + 8 - pre8;
+#ifndef LSBM_ABL_U_NOFIX
+    c0 ^= dx;
+    c1 ^= dy;
+    c2 ^= dz;
+    c3 ^= dw;
+#endif
+    // this round becomes the previous one
+#if defined(LSBM_ABL_U_NOMERGE)  // diagnostic builds only (wrong CRCs)
+    p0 = c0 ^ c1 ^ c2 ^ c3;
+    p1 = p2 = p3 = 0;
+#else
+    p0 = c0;
+    p1 = c1;
+    p2 = c2;
+    p3 = c3;
+#endif
+#if defined(LSBM_ABL_U_NOSHIFT) || defined(LSBM_ABL_U_NOMERGE)
+    pk = 0;
+#else
+    pk = k;
+#endif
+    pb = b;
+    pact = active;
+    rj = rn;
+    ivj = ivn;
+    cur_b = nb;
+    cur_o = no;
   }
+  retire();
 }
 
 // One thread per block: acc -> CRC -> output mode.

@@ -18,7 +18,8 @@ constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
 constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
                                          // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
 constexpr uint32_t kNibU4096 = kNibFin + 8 * 16 * 32 * 4;  // A^(4096 * 2^i), i = 0..15
-constexpr uint32_t kLdsBytes = kNibU4096 + 16 * 512;
+constexpr uint32_t kNibNeg4 = kNibU4096 + 16 * 512;  // A^-4 (init injection)
+constexpr uint32_t kLdsBytes = kNibNeg4 + 512;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
 // Tables in device global memory, built once per device by the host (gf2.h).
