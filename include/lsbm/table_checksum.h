@@ -15,8 +15,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include <string>
 #include <vector>
+
+#include "lsbm/status.h"
 
 namespace lsbm {
 
@@ -31,25 +32,6 @@ enum CompressionType : uint8_t { kNoCompression = 0x0, kSnappyCompression = 0x1 
 
 // table/format.h:84
 static const size_t kBlockTrailerSize = 5;
-
-// The subset of leveldb::Status (include/leveldb/status.h) this layer returns.
-class Status {
- public:
-  Status() : code_(kOk) {}
-  static Status OK() { return Status(); }
-  static Status Corruption(const std::string& msg) { return Status(kCorruption, msg); }
-  static Status InvalidArgument(const std::string& msg) { return Status(kInvalidArgument, msg); }
-  static Status IOError(const std::string& msg) { return Status(kIOError, msg); }
-  bool ok() const { return code_ == kOk; }
-  bool IsCorruption() const { return code_ == kCorruption; }
-  std::string ToString() const;
-
- private:
-  enum Code { kOk = 0, kCorruption = 2, kInvalidArgument = 4, kIOError = 5 };
-  Status(Code c, const std::string& m) : code_(c), msg_(m) {}
-  Code code_;
-  std::string msg_;
-};
 
 // Lay n blocks of the given sizes back to back, each followed by its 5-byte
 // trailer (offset += size + kBlockTrailerSize, table/table_builder.cc:251).

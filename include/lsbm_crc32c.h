@@ -22,6 +22,10 @@
  *   table/format.cc:95-103   ReadBlock's verify_checksums compare
  *                            -> lsbm_sst_verify_dev
  *   table/format.h:84        kBlockTrailerSize = 5 -> LSBM_BLOCK_TRAILER_SIZE
+ *   common/log_writer.cc:75-100  log::Writer::EmitPhysicalRecord header CRC
+ *                            -> lsbm_log_seal_dev
+ *   common/log_reader.cc:228-242 log::Reader::ReadPhysicalRecord checksum
+ *                            -> lsbm_log_verify_dev
  */
 #ifndef LSBM_CRC32C_H_
 #define LSBM_CRC32C_H_
@@ -101,6 +105,26 @@ int lsbm_sst_seal_dev(uint8_t* d_file, const uint64_t* d_handles, const uint8_t*
  * added to *d_nbad when non-NULL. */
 int lsbm_sst_verify_dev(const uint8_t* d_file, const uint64_t* d_handles, uint64_t n_blocks,
                         uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+
+/* ---- WAL / MANIFEST log records over a device-resident log image ----
+ * common/log_format.h: 32 KiB log blocks of physical records, each a 7-byte
+ * header [masked crc LE32][length LE16][type u8] followed by `length` payload
+ * bytes.  d_headers[i] is the byte offset of record i's header in d_log
+ * (log_bytes long); the CRC covers [type || payload] = header[6, 7 + length).
+ * A record whose header or payload does not fit inside log_bytes is counted
+ * into *d_nbad (when non-NULL) and never read past the image. */
+/* log::Writer::EmitPhysicalRecord (common/log_writer.cc:75-100): with length
+ * and type already in place, writes header[0, 4) =
+ * EncodeFixed32(Mask(Extend(type_crc_[type], payload, length))), which equals
+ * Mask(Value(header + 6, 1 + length)); d_masked (nullable) receives the same
+ * masked values.  Records that do not fit are left untouched (d_masked 0). */
+int lsbm_log_seal_dev(uint8_t* d_log, uint64_t log_bytes, const uint64_t* d_headers,
+                      uint64_t n_records, uint32_t* d_masked, uint32_t* d_nbad, void* stream);
+/* log::Reader::ReadPhysicalRecord's checksum (common/log_reader.cc:228-242):
+ * d_ok[i] = 1 iff the record fits and
+ * Unmask(DecodeFixed32(header)) == Value(header + 6, 1 + length). */
+int lsbm_log_verify_dev(const uint8_t* d_log, uint64_t log_bytes, const uint64_t* d_headers,
+                        uint64_t n_records, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
 
 /* ---- host-staged batch (blocks start and end in host memory) ----
  * Same contract as lsbm_crc32c_batch_dev but every pointer is a host pointer

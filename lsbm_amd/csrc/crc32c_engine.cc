@@ -421,6 +421,49 @@ __attribute__((visibility("default"))) int lsbm_sst_verify_dev(const uint8_t* d_
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
+__attribute__((visibility("default"))) int lsbm_log_seal_dev(uint8_t* d_log, uint64_t log_bytes,
+                                                             const uint64_t* d_headers,
+                                                             uint64_t n_records,
+                                                             uint32_t* d_masked, uint32_t* d_nbad,
+                                                             void* stream) {
+  if (n_records == 0) return LSBM_OK;
+  if (!d_log || !d_headers) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_log;
+  a.file = d_log;
+  a.handles = d_headers;
+  a.extents = kExtLogHeaders;
+  a.limit = log_bytes;
+  a.n = n_records;
+  a.out = d_masked;
+  a.nbad = d_nbad;
+  a.mode = kModeLogSeal;
+  a.dbg_lo = reinterpret_cast<uint64_t>(d_log);
+  a.dbg_hi = a.dbg_lo + log_bytes;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_log_verify_dev(const uint8_t* d_log,
+                                                               uint64_t log_bytes,
+                                                               const uint64_t* d_headers,
+                                                               uint64_t n_records, uint8_t* d_ok,
+                                                               uint32_t* d_nbad, void* stream) {
+  if (n_records == 0) return LSBM_OK;
+  if (!d_log || !d_headers || !d_ok) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_log;
+  a.handles = d_headers;
+  a.extents = kExtLogHeaders;
+  a.limit = log_bytes;
+  a.n = n_records;
+  a.ok = d_ok;
+  a.nbad = d_nbad;
+  a.mode = kModeLogVerify;
+  a.dbg_lo = reinterpret_cast<uint64_t>(d_log);
+  a.dbg_hi = a.dbg_lo + log_bytes;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
 __attribute__((visibility("default"))) int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes,
                                                                     uint64_t seed, void* stream) {
   if (nbytes == 0) return LSBM_OK;

@@ -221,10 +221,26 @@ struct ExtRaw {
 };
 typedef const __attribute__((address_space(1))) uint64_t* gptr_u64;
 typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;
+typedef const __attribute__((address_space(1))) uint8_t* gptr_u8;
+
+constexpr uint64_t kLogHeaderSize = 7;  // common/log_format.h:30 (crc 4, length 2, type 1)
+constexpr uint64_t kLogNoHeader = ~0ull;  // ExtRaw.y of a header that is not inside the image
 
 __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) {
   ExtRaw r = {0, 0};
-  if (a.extents == kExtHandles) {
+  if (a.extents == kExtLogHeaders) {
+    // header offset, then the record length (LE16 at h + 4) read byte-wise;
+    // a header that does not fit the image reads the zero pad instead
+    const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
+    r.x = h[b];
+    const bool inside = r.x <= a.limit && a.limit - r.x >= kLogHeaderSize;
+    uint64_t p = inside ? reinterpret_cast<uint64_t>(a.base) + r.x + 4
+                        : reinterpret_cast<uint64_t>(a.dc->zero16);
+    asm volatile("" : "+v"(p));  // defined in every lane (see crc32c_units_kernel)
+    const gptr_u8 q = reinterpret_cast<gptr_u8>(p);
+    const uint64_t len = (uint64_t)q[0] | ((uint64_t)q[1] << 8);
+    r.y = inside ? len : kLogNoHeader;
+  } else if (a.extents == kExtHandles) {
     const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
     r.x = h[2 * b];
     r.y = h[2 * b + 1];
@@ -236,11 +252,22 @@ __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) 
   return r;
 }
 
+// A log record's header and payload lie inside the image [0, limit).
+__device__ __forceinline__ bool log_record_fits(const RaggedArgs& a, ExtRaw r) {
+  return r.y != kLogNoHeader && a.limit - r.x - kLogHeaderSize >= r.y;
+}
+
 // Block b's extent [s, e) as absolute addresses.
 __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b, ExtRaw r,
                                                 uint64_t& s, uint64_t& e) {
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
-  if (a.extents == kExtHandles) {
+  if (a.extents == kExtLogHeaders) {
+    // CRC over [type || payload] = [h + 6, h + 7 + length) (common/log_reader.cc:231);
+    // a record that does not fit the image is empty here and bad in the finish kernel
+    const bool fits = log_record_fits(a, r);
+    s = base + (fits ? r.x + 6 : 0);
+    e = fits ? s + 1 + r.y : s;
+  } else if (a.extents == kExtHandles) {
     s = base + r.x;
     e = s + r.y + (a.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
   } else if (a.extents == kExtFixed) {
@@ -267,12 +294,6 @@ __device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e) {
   f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
   f.units = (uint32_t)((f.rows + kUnitRows - 1) / kUnitRows);
   return f;
-}
-
-__device__ __forceinline__ Frame block_frame(const RaggedArgs& a, uint64_t b) {
-  uint64_t s, e;
-  extent_from_raw(a, b, load_ext_raw(a, b), s, e);
-  return frame_of(s, e);
 }
 
 // M(v) for nibble tables in LDS at byte offset `tab` (low 6 bits clear).
@@ -585,7 +606,10 @@ __global__ __launch_bounds__(256) void crc32c_finish_kernel(RaggedArgs args) {
   const DevConsts* __restrict__ dc = args.dc;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < args.n;
        b += (uint64_t)gridDim.x * blockDim.x) {
-    const Frame f = block_frame(args, b);
+    const ExtRaw raw = load_ext_raw(args, b);
+    uint64_t s0, e0;
+    extent_from_raw(args, b, raw, s0, e0);
+    const Frame f = frame_of(s0, e0);
     const uint32_t z = (uint32_t)((f.row0 + f.rows) * kRowBytes - f.e);
 #ifdef LSBM_DEBUG_BOUNDS
     if (z >= 128) { printf("Z OOB b %lu z %u s %lx e %lx row0 %lx rows %lu\n", (unsigned long)b, z, (unsigned long)f.s, (unsigned long)f.e, (unsigned long)f.row0, (unsigned long)f.rows); continue; }
@@ -615,6 +639,33 @@ __global__ __launch_bounds__(256) void crc32c_finish_kernel(RaggedArgs args) {
         t[2] = (uint8_t)(m >> 8);
         t[3] = (uint8_t)(m >> 16);
         t[4] = (uint8_t)(m >> 24);
+        break;
+      }
+      case kModeLogSeal: {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
+        if (!log_record_fits(args, raw)) {
+          if (args.out) args.out[b] = 0;
+          if (args.nbad) atomicAdd(args.nbad, 1u);
+          break;
+        }
+        uint8_t* h = args.file + raw.x;
+        const uint32_t m = mask_crc(crc);
+        h[0] = (uint8_t)m;
+        h[1] = (uint8_t)(m >> 8);
+        h[2] = (uint8_t)(m >> 16);
+        h[3] = (uint8_t)(m >> 24);
+        if (args.out) args.out[b] = m;
+        break;
+      }
+      case kModeLogVerify: {  // log::Reader::ReadPhysicalRecord, common/log_reader.cc:228-242
+        bool good = false;
+        if (log_record_fits(args, raw)) {
+          const uint8_t* h = args.base + raw.x;
+          const uint32_t stored = (uint32_t)h[0] | ((uint32_t)h[1] << 8) |
+                                  ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+          good = unmask_crc(stored) == crc;
+        }
+        args.ok[b] = good ? 1 : 0;
+        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
         break;
       }
       default: {  // kModeSstVerify: table/format.cc:95-103

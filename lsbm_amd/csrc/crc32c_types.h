@@ -41,6 +41,8 @@ enum ExtentKind : uint32_t {
   kExtOffsets = 0,  // [offsets[i], offsets[i+1])
   kExtHandles = 1,  // [h[2i], h[2i] + h[2i+1])  (BlockHandle {offset, size})
   kExtFixed = 2,    // [i*stride, i*stride + len)
+  kExtLogHeaders = 3,  // log record at h = headers[i]: [h + 6, h + 7 + length) where
+                       // length = LE16 at h + 4 (common/log_format.h, 7-byte header)
 };
 
 enum RaggedMode : uint32_t {
@@ -48,6 +50,8 @@ enum RaggedMode : uint32_t {
   kModeVerify = 1,     // ok[i] = (crc == expect[i]); mismatches added to *nbad
   kModeSstSeal = 2,    // write trailer [type][Mask(crc(block || type))] after the block
   kModeSstVerify = 3,  // ok[i] = stored trailer == Mask(crc(block || type))
+  kModeLogSeal = 4,    // header[0..4) = Mask(crc(type || payload)); out[i] too if non-null
+  kModeLogVerify = 5,  // ok[i] = Unmask(header[0..4)) == crc(type || payload)
 };
 
 // Ragged path: a block's 128-B-aligned frame [row0, row_end) is cut into
@@ -74,6 +78,7 @@ struct RaggedArgs {
   uint32_t extents;
   const DevConsts* dc;
   uint32_t* acc;         // n per-block accumulators (zeroed before the units kernel)
+  uint64_t limit;        // kExtLogHeaders: image size; records past it are empty + bad
   uint64_t dbg_lo, dbg_hi;  // LSBM_DEBUG_BOUNDS builds: the valid data range
 };
 

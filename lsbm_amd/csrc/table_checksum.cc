@@ -8,17 +8,9 @@
 #include <string.h>
 
 #include "../../include/lsbm_crc32c.h"
+#include "host_stage.h"
 
 namespace lsbm {
-
-std::string Status::ToString() const {
-  switch (code_) {
-    case kOk: return "OK";
-    case kCorruption: return "Corruption: " + msg_;
-    case kInvalidArgument: return "Invalid argument: " + msg_;
-    default: return "IO error: " + msg_;
-  }
-}
 
 std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64_t* file_size) {
   std::vector<BlockHandle> h(sizes.size());
@@ -38,7 +30,10 @@ struct DeviceBuffers {
   uint64_t* handles = nullptr;
   uint8_t* aux = nullptr;   // types (seal) or ok flags (verify)
   uint32_t* nbad = nullptr;
+  PinnedBounce bounce;
+  CallStream stream;
   ~DeviceBuffers() {
+    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
     if (file) (void)hipFree(file);
     if (handles) (void)hipFree(handles);
     if (aux) (void)hipFree(aux);
@@ -58,21 +53,22 @@ Status check_handles(size_t file_size, const BlockHandle* h, size_t n) {
   return Status::OK();
 }
 
-// Stage file + handles (+ aux bytes) on `device`.
+// Stage file + handles (+ aux bytes) on `device` (host_stage.h).
 Status stage(int device, const void* file, size_t file_size, const BlockHandle* h, size_t n,
              const uint8_t* aux_in, DeviceBuffers* d) {
   int rc = lsbm_crc32c_init(device);
   if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
   hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = d->stream.status();
   if (e == hipSuccess) e = hipMalloc(&d->file, file_size ? file_size : 1);
   if (e == hipSuccess) e = hipMalloc(&d->handles, n * sizeof(BlockHandle));
   if (e == hipSuccess) e = hipMalloc(&d->aux, n);
   if (e == hipSuccess) e = hipMalloc(&d->nbad, sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemcpy(d->file, file, file_size, hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipMemcpy(d->handles, h, n * sizeof(BlockHandle), hipMemcpyHostToDevice);  // {offset,size}
-  if (e == hipSuccess && aux_in) e = hipMemcpy(d->aux, aux_in, n, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(d->nbad, 0, sizeof(uint32_t));
+  hipStream_t s = d->stream.get();
+  if (e == hipSuccess) e = d->bounce.to_device(d->file, file, file_size, s);
+  if (e == hipSuccess) e = d->bounce.to_device(d->handles, h, n * sizeof(BlockHandle), s);  // {offset,size}
+  if (e == hipSuccess && aux_in) e = d->bounce.to_device(d->aux, aux_in, n, s);
+  if (e == hipSuccess) e = hipMemsetAsync(d->nbad, 0, sizeof(uint32_t), s);
   return e == hipSuccess ? Status::OK() : hip_status(e, "staging");
 }
 
@@ -87,16 +83,23 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
   DeviceBuffers d;
   s = stage(device, file, file_size, handles, n, types, &d);
   if (!s.ok()) return s;
-  if (lsbm_sst_seal_dev(d.file, d.handles, d.aux, n, nullptr) != LSBM_OK)
+  if (lsbm_sst_seal_dev(d.file, d.handles, d.aux, n, d.stream.get()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
-  hipError_t e = hipDeviceSynchronize();
-  // bring back only the trailers
+  // bring back only the trailers: gather them on the device side of the
+  // bounce, one 5-byte piece per block
+  std::vector<uint8_t> trailers(n * kBlockTrailerSize);
+  hipError_t e = hipSuccess;
   for (size_t i = 0; e == hipSuccess && i < n; i++) {
     const uint64_t t = handles[i].offset + handles[i].size;
-    e = hipMemcpyAsync(file + t, d.file + t, kBlockTrailerSize, hipMemcpyDeviceToHost, nullptr);
+    e = hipMemcpyAsync(trailers.data() + i * kBlockTrailerSize, d.file + t, kBlockTrailerSize,
+                       hipMemcpyDeviceToHost, d.stream.get());
   }
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  return e == hipSuccess ? Status::OK() : hip_status(e, "seal");
+  if (e == hipSuccess) e = hipStreamSynchronize(d.stream.get());
+  if (e != hipSuccess) return hip_status(e, "seal");
+  for (size_t i = 0; i < n; i++)
+    memcpy(file + handles[i].offset + handles[i].size, trailers.data() + i * kBlockTrailerSize,
+           kBlockTrailerSize);
+  return Status::OK();
 }
 
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
@@ -109,11 +112,11 @@ Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockH
   DeviceBuffers d;
   s = stage(device, file, file_size, handles, n, nullptr, &d);
   if (!s.ok()) return s;
-  if (lsbm_sst_verify_dev(d.file, d.handles, n, d.aux, d.nbad, nullptr) != LSBM_OK)
+  if (lsbm_sst_verify_dev(d.file, d.handles, n, d.aux, d.nbad, d.stream.get()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
   uint32_t nbad = 0;
-  hipError_t e = hipMemcpy(&nbad, d.nbad, sizeof(nbad), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && ok) e = hipMemcpy(ok->data(), d.aux, n, hipMemcpyDeviceToHost);
+  hipError_t e = d.bounce.to_host(&nbad, d.nbad, sizeof(nbad), d.stream.get());
+  if (e == hipSuccess && ok) e = d.bounce.to_host(ok->data(), d.aux, n, d.stream.get());
   if (e != hipSuccess) return hip_status(e, "verify");
   return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
 }
