@@ -24,7 +24,7 @@ LSBM_CRC32C_MASKED = 0x1
 LSBM_CRC32C_MASK_DELTA = 0xA282EAD8
 LSBM_BLOCK_TRAILER_SIZE = 5
 
-# every symbol include/lsbm_crc32c.h declares: name -> (restype, argtypes)
+# every symbol include/lsbm_crc32c.h and include/lsbm_bloom.h declare: name -> (restype, argtypes)
 _u32, _u64, _int, _vp, _sz = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
                               ctypes.c_void_p, ctypes.c_size_t)
 SIGNATURES = {
@@ -46,6 +46,16 @@ SIGNATURES = {
     "lsbm_crc32c_batch_host": (_int, [_int, _vp, _vp, _u64, _vp, _vp, _u32]),
     "lsbm_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),
     "lsbm_stream_read_dev": (_int, [_vp, _u64, _vp, _vp]),
+    # include/lsbm_bloom.h
+    "lsbm_bloom_hash": (_u32, [_vp, _sz, _u32]),
+    "lsbm_bloom_filter_bytes": (_u64, [_u64, _int]),
+    "lsbm_bloom_k": (_u32, [_int]),
+    "lsbm_bloom_k_probe": (_u64, [_int, _int]),
+    "lsbm_bloom_build_dev": (_int, [_vp, _vp, _u32, _vp, _vp, _u64, _int, _vp, _vp]),
+    "lsbm_bloom_may_match_dev": (_int, [_vp, _vp, _vp, _vp, _u32, _u64, _int, _int, _vp, _vp,
+                                        _vp]),
+    "lsbm_filter_block_may_match_dev": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u64, _int, _int,
+                                               _vp, _vp, _vp]),
 }
 
 _lib = None

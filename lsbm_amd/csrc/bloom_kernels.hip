@@ -1,0 +1,251 @@
+// bloom_kernels.hip -- gfx950 kernels of the batched bloom-filter engine
+// (include/lsbm_bloom.h).
+//
+// bloom_build_kernel  CreateFilter (util/bloom.cc:37-63) for many filters:
+//                     one wave per filter.  The wave's lanes hash one key
+//                     each and set the key's k bits with ds_or_b32 in the
+//                     wave's LDS slice; the finished bit array leaves LDS once,
+//                     as dword stores (byte stores at the two unaligned ends,
+//                     which may share a dword with a neighbouring filter).
+//                     Filters wider than the slice are built window by window
+//                     (every key re-hashed per window; rare: > 1,600 keys at
+//                     20 bits/key).  No global atomics, no zero-fill pass.
+// bloom_probe_kernel  KeyMayMatch (util/bloom.cc:65-89) for many lookups, one
+//                     lane per lookup, optionally through FilterBlockReader's
+//                     offset array (table/filter_block.cc:78-109).
+//
+// Both hash exactly as util/hash.cc:18-49, signed-char tail included, and
+// take bitpos = h % bits as util/bloom.cc:58/84 do (32-bit h, size_t bits).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bloom_types.h"
+
+namespace lsbm {
+namespace {
+
+typedef const __attribute__((address_space(1))) uint32_t* gcu32;
+typedef const __attribute__((address_space(1))) uint8_t* gcu8;
+typedef __attribute__((address_space(1))) uint32_t* gu32;
+typedef __attribute__((address_space(1))) uint8_t* gu8;
+
+constexpr uint32_t kHashM = 0xc6a4a793u;     // util/hash.cc:20
+constexpr uint32_t kBloomSeed = 0xbc9f1d34u;  // util/bloom.cc:14
+
+// A `char` of util/hash.cc:37-43, promoted to int and then to uint32_t.
+__device__ __forceinline__ uint32_t sext8(uint32_t b) { return (uint32_t)(int32_t)(int8_t)(uint8_t)b; }
+
+// util/hash.cc:18-49 over global bytes [s, s + n), any alignment.  Words are
+// read aligned and funnel-shifted (v_alignbyte); only words that overlap the
+// key are read, so a key ending at a page boundary never touches the next page.
+__device__ uint32_t hash_key(uint64_t s, uint64_t n, uint32_t seed) {
+  uint32_t h = seed ^ (uint32_t)(n * kHashM);
+  if (n == 0) return h;
+  const uint64_t w_last = (s + n - 1) & ~3ull;
+  const uint32_t sh = (uint32_t)s & 3u;
+  uint64_t q = s & ~3ull;
+  uint32_t lo = *reinterpret_cast<gcu32>(q);
+  for (uint64_t k = n >> 2; k; k--) {
+    q += 4;
+    const uint32_t hi = *reinterpret_cast<gcu32>(q < w_last ? q : w_last);
+    h += __builtin_amdgcn_alignbyte(hi, lo, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    lo = hi;
+  }
+  const uint32_t r = (uint32_t)n & 3u;
+  if (r) {
+    q += 4;
+    const uint32_t hi = *reinterpret_cast<gcu32>(q < w_last ? q : w_last);
+    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    if (r == 3) h += sext8(w >> 16) << 16;
+    if (r >= 2) h += sext8(w >> 8) << 8;
+    h += sext8(w);
+    h *= kHashM;
+    h ^= h >> 24;
+  }
+  return h;
+}
+
+// Key i of a batch: [keys + off[i], keys + off[i+1] - strip); empty when the
+// key is shorter than strip (ExtractUserKey asserts >= 8, common/dbformat.h:76).
+__device__ __forceinline__ void key_extent(const uint8_t* keys, const uint64_t* offs, uint64_t i,
+                                           uint32_t strip, uint64_t& s, uint64_t& n) {
+  const uint64_t a = offs[i], b = offs[i + 1];
+  s = reinterpret_cast<uint64_t>(keys) + a;
+  n = b >= a + strip ? b - a - strip : 0;
+}
+
+// h % bits for a filter of `bits` bits (util/bloom.cc:58, :84): h is 32-bit and
+// bits a size_t, so the result is h itself once bits >= 2^32.  A double multiply
+// by the filter's reciprocal gives the quotient to within 2^-23 (h < 2^32,
+// bits >= 8), and one +-bits step makes the remainder exact.
+struct BitMod {
+  double rcp;
+  uint32_t d;
+  bool big;
+};
+
+__device__ __forceinline__ BitMod bit_mod(uint64_t bits) {
+  BitMod m;
+  m.big = bits > 0xffffffffull;
+  m.d = m.big ? 1u : (uint32_t)bits;
+  m.rcp = 1.0 / (double)m.d;
+  return m;
+}
+
+__device__ __forceinline__ uint32_t mod_bits(uint32_t h, const BitMod& m) {
+  if (m.big) return h;
+  const uint32_t q = (uint32_t)((double)h * m.rcp);
+  int64_t r = (int64_t)h - (int64_t)q * (int64_t)m.d;
+  if (r < 0) r += m.d;
+  else if (r >= (int64_t)m.d) r -= m.d;
+  return (uint32_t)r;
+}
+
+// Orders one wave's LDS phases (its own ds ops complete in order; this keeps
+// the compiler from moving accesses across the phase boundary).
+__device__ __forceinline__ void wave_phase() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// LDS bytes [0, n) of the wave's slice -> global [d, d + n), any alignment.
+// The aligned middle goes out as dwords (64 lanes x 4 B per instruction); the
+// up to 3 + 3 bytes at the ends as byte stores, which leave the bytes of a
+// neighbouring filter in the same dword alone.
+__device__ __forceinline__ void store_window(uint64_t d, const uint32_t* bm, uint32_t n,
+                                             uint32_t lane) {
+  const uint8_t* b8 = reinterpret_cast<const uint8_t*>(bm);
+  uint32_t head = (4u - ((uint32_t)d & 3u)) & 3u;
+  if (head > n) head = n;
+  const uint32_t body = (n - head) >> 2;
+  const uint32_t tail0 = head + 4 * body;
+  if (lane < head) *reinterpret_cast<gu8>(d + lane) = b8[lane];
+  if (lane < n - tail0) *reinterpret_cast<gu8>(d + tail0 + lane) = b8[tail0 + lane];
+  // source bytes of output dword i: [head + 4i, head + 4i + 4) = words i, i+1
+  for (uint32_t i = lane; i < body; i += 64)
+    *reinterpret_cast<gu32>(d + head + 4ull * i) = __builtin_amdgcn_alignbyte(bm[i + 1], bm[i], head);
+}
+
+__global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildArgs a) {
+  __shared__ uint32_t lds[kBloomWaves][kBloomWindowWords + 1];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* bm = lds[wv];
+  const uint64_t nwaves = (uint64_t)gridDim.x * kBloomWaves;
+  for (uint64_t f = (uint64_t)blockIdx.x * kBloomWaves + wv; f < a.n_filters; f += nwaves) {
+    // util/bloom.cc:39-46: bits = max(64, n * bits_per_key), rounded up to bytes
+    const uint64_t k0 = a.filter_first[f], k1 = a.filter_first[f + 1];
+    const uint64_t nk = k1 > k0 ? k1 - k0 : 0;
+    uint64_t bits = nk * a.bits_per_key;
+    if (bits < 64) bits = 64;
+    const uint64_t bytes = (bits + 7) / 8;
+    const BitMod m = bit_mod(bytes * 8);
+    const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + a.filter_out[f];
+    for (uint64_t win = 0; win < bytes; win += kBloomWindowBytes) {
+      const uint32_t wbytes =
+          (uint32_t)(bytes - win < kBloomWindowBytes ? bytes - win : kBloomWindowBytes);
+      const uint64_t bit0 = win * 8, nbits = (uint64_t)wbytes * 8;
+      for (uint32_t i = lane; i <= wbytes / 4; i += 64) bm[i] = 0;  // + 1 pad word
+      wave_phase();
+      // util/bloom.cc:52-62: double hashing, delta = h rotated right 17
+      for (uint64_t i = k0 + lane; i < k1; i += 64) {
+        uint64_t s, n;
+        key_extent(a.keys, a.key_offsets, i, a.strip, s, n);
+        uint32_t h = hash_key(s, n, kBloomSeed);
+        const uint32_t delta = (h >> 17) | (h << 15);
+        for (uint32_t j = 0; j < a.k; j++) {
+          const uint64_t rel = (uint64_t)mod_bits(h, m) - bit0;  // wraps below the window
+          if (rel < nbits) atomicOr(&bm[rel >> 5], 1u << (rel & 31u));
+          h += delta;
+        }
+      }
+      wave_phase();
+      store_window(dst + win, bm, wbytes, lane);
+      wave_phase();
+    }
+    if (lane == 0) *reinterpret_cast<gu8>(dst + bytes) = (uint8_t)a.k;  // :50
+  }
+}
+
+__device__ __forceinline__ uint64_t load_le32(uint64_t p) {  // DecodeFixed32, any alignment
+  const gcu8 b = reinterpret_cast<gcu8>(p);
+  return (uint64_t)b[0] | ((uint64_t)b[1] << 8) | ((uint64_t)b[2] << 16) | ((uint64_t)b[3] << 24);
+}
+
+// util/bloom.cc:65-89 on the filter [f, f + len).
+__device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn,
+                              uint64_t k_use) {
+  if (len < 2) return false;
+  // `array[len-1] > k_use_`: a signed char converted to size_t
+  const uint64_t stored = (uint64_t)(int64_t)(int8_t)*reinterpret_cast<gcu8>(f + len - 1);
+  const uint64_t k = stored > k_use ? k_use : stored;
+  if (k > 30) return true;
+  const BitMod m = bit_mod((len - 1) * 8);
+  uint32_t h = hash_key(ks, kn, kBloomSeed);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (uint32_t j = 0; j < (uint32_t)k; j++) {
+    const uint32_t bitpos = mod_bits(h, m);
+    if ((*reinterpret_cast<gcu8>(f + (bitpos >> 3)) & (1u << (bitpos & 7u))) == 0) return false;
+    h += delta;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bloom_probe_kernel(BloomProbeArgs a) {
+  uint32_t hits = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += stride) {
+    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * q];
+    const uint64_t size = a.handles[2 * q + 1];
+    uint64_t ks, kn;
+    key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
+    bool may;
+    if (a.mode == kProbeFilter) {
+      may = key_may_match(c, size, ks, kn, a.k_use);
+    } else {
+      // FilterBlockReader (table/filter_block.cc:78-109): "errors are treated
+      // as potential matches"; base_lg is a size_t loaded from a char, and the
+      // shift count is taken mod 64 as on the x86-64 reference build
+      may = true;
+      if (size >= 5) {
+        const uint64_t base_lg = (uint64_t)(int64_t)(int8_t)*reinterpret_cast<gcu8>(c + size - 1);
+        const uint64_t last_word = load_le32(c + size - 5);
+        if (last_word <= size - 5) {
+          const uint64_t num = (size - 5 - last_word) / 4;
+          const uint64_t index = a.data_offsets[q] >> (base_lg & 63u);
+          if (index < num) {
+            const uint64_t start = load_le32(c + last_word + index * 4);
+            const uint64_t limit = load_le32(c + last_word + index * 4 + 4);
+            if (start <= limit && limit <= last_word)
+              may = key_may_match(c + start, limit - start, ks, kn, a.k_use);
+            else if (start == limit)
+              may = false;  // an empty filter matches nothing
+          }
+        }
+      }
+    }
+    a.may[q] = may ? 1 : 0;
+    hits += may ? 1u : 0u;
+  }
+  if (a.n_may) {  // one atomic per wave
+    for (int o = 32; o; o >>= 1) hits += (uint32_t)__shfl_xor((int)hits, o);
+    if ((threadIdx.x & 63u) == 0 && hits) atomicAdd(a.n_may, hits);
+  }
+}
+
+}  // namespace
+
+// ---- host-callable launchers (used by bloom_engine.cc) ----
+hipError_t launch_bloom_build(const BloomBuildArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(bloom_build_kernel, dim3(grid), dim3(kBloomThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bloom_probe(const BloomProbeArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(bloom_probe_kernel, dim3(grid), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace lsbm

@@ -18,6 +18,7 @@
 
 #include "../../include/lsbm_crc32c.h"
 #include "crc32c_types.h"
+#include "engine_internal.h"
 #include "gf2.h"
 
 namespace lsbm {
@@ -275,6 +276,17 @@ void gather_blocks(uint8_t* dst, const uint64_t* rebased, const uint8_t* src,
 }
 
 }  // namespace
+
+// engine_internal.h: shared with the bloom entry points (bloom_engine.cc)
+int engine_fail(int code, const char* what) { return fail(code, what); }
+int engine_fail_hip(hipError_t e, const char* what) { return fail_hip(e, what); }
+int engine_current_cus(int* cus) {
+  DeviceState* st = nullptr;
+  const int rc = current_device(&st);
+  if (rc == LSBM_OK) *cus = st->num_cus;
+  return rc;
+}
+
 }  // namespace lsbm
 
 using namespace lsbm;

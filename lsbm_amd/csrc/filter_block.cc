@@ -1,0 +1,192 @@
+// filter_block.cc -- include/lsbm/filter_block.h on top of the C ABI.
+//
+// Builder: the reference's layout decisions (which keys form which filter,
+// table/filter_block.cc:22-28, 52-76) are made on the host as keys arrive;
+// they depend only on block offsets and key counts, so the whole block layout
+// is known before any hashing.  Finish stages every builder's keys once, runs
+// one lsbm_bloom_build_dev over all their filters, and appends the offset
+// array, array_offset and base_lg (:41-49) on the host.
+#include "../../include/lsbm/filter_block.h"
+
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+
+#include "../../include/lsbm_bloom.h"
+#include "host_stage.h"
+
+namespace lsbm {
+
+namespace {
+
+constexpr uint64_t kFilterBase = 1ull << LSBM_FILTER_BASE_LG;  // table/filter_block.cc:14-16
+
+Status hip_status(hipError_t e, const char* what) {
+  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void put_fixed32(std::string* dst, uint32_t v) {  // util/coding.cc PutFixed32
+  const char b[4] = {(char)(v & 0xff), (char)((v >> 8) & 0xff), (char)((v >> 16) & 0xff),
+                     (char)(v >> 24)};
+  dst->append(b, 4);
+}
+
+// Device buffers of one call, freed after the stream drains.
+struct DeviceArena {
+  std::vector<void*> ptrs;
+  PinnedBounce bounce;
+  CallStream stream;
+  ~DeviceArena() {
+    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <typename T>
+  hipError_t alloc(T** p, size_t count) {
+    void* q = nullptr;
+    const hipError_t e = hipMalloc(&q, count ? count * sizeof(T) : 1);
+    if (e == hipSuccess) ptrs.push_back(q);
+    *p = static_cast<T*>(q);
+    return e;
+  }
+  template <typename T>
+  hipError_t upload(T** d, const T* h, size_t count) {
+    hipError_t e = alloc(d, count);
+    if (e == hipSuccess && count) e = bounce.to_device(*d, h, count * sizeof(T), stream.get());
+    return e;
+  }
+};
+
+Status prepare(int device, DeviceArena* a) {
+  if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = a->stream.status();
+  return e == hipSuccess ? Status::OK() : hip_status(e, "device");
+}
+
+}  // namespace
+
+FilterBlockBuilder::FilterBlockBuilder(const BloomOptions& options)
+    : options_(options), pending_(0) {}
+
+void FilterBlockBuilder::StartBlock(uint64_t block_offset) {
+  const uint64_t filter_index = block_offset / kFilterBase;
+  while (filter_index > filters_.size()) GenerateFilter();
+}
+
+void FilterBlockBuilder::AddKey(const char* key, size_t n) {
+  starts_.push_back(keys_.size());
+  keys_.append(key, n);
+}
+
+void FilterBlockBuilder::GenerateFilter() {
+  filters_.push_back(Range{pending_, (uint64_t)starts_.size()});
+  pending_ = starts_.size();
+}
+
+Status FilterBlockBuilder::Finish(int device, std::string* result) {
+  FilterBlockBuilder* self = this;
+  return FinishFilterBlocks(device, &self, 1, result);
+}
+
+Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_t n,
+                          std::string* results) {
+  if (n == 0) return Status::OK();
+  const int bpk = builders[0]->options_.bits_per_key;
+  const bool internal = builders[0]->options_.internal_keys;
+  if (bpk < 0) return Status::InvalidArgument("bits_per_key < 0");
+  // host layout of every block
+  std::string keys;
+  std::vector<uint64_t> key_offs, first, out_off;
+  std::vector<uint64_t> data_base(n), data_size(n);
+  std::vector<std::vector<uint32_t>> offsets(n);
+  uint64_t out_total = 0;
+  for (size_t t = 0; t < n; t++) {
+    FilterBlockBuilder& b = *builders[t];
+    if (b.options_.bits_per_key != bpk || b.options_.internal_keys != internal)
+      return Status::InvalidArgument("one bits_per_key and key kind per batch");
+    if (b.pending_ < b.starts_.size()) b.GenerateFilter();  // Finish, :37-39
+    const uint64_t key_base = key_offs.size(), byte_base = keys.size();
+    for (uint64_t s : b.starts_) key_offs.push_back(byte_base + s);
+    keys += b.keys_;
+    uint64_t size = 0;
+    for (const auto& r : b.filters_) {
+      offsets[t].push_back((uint32_t)size);  // filter_offsets_ (:56, :70)
+      if (r.hi > r.lo) {
+        first.push_back(key_base + r.lo);
+        out_off.push_back(out_total + size);
+        size += lsbm_bloom_filter_bytes(r.hi - r.lo, bpk);
+      }
+    }
+    data_base[t] = out_total;
+    data_size[t] = size;
+    out_total += size;
+  }
+  key_offs.push_back(keys.size());
+  first.push_back(key_offs.size() - 1);  // filters cover every key, in order
+  std::vector<char> data(out_total);
+  const size_t nf = out_off.size();
+  if (nf) {
+    DeviceArena a;
+    Status s = prepare(device, &a);
+    if (!s.ok()) return s;
+    uint8_t *d_keys = nullptr, *d_out = nullptr;
+    uint64_t *d_offs = nullptr, *d_first = nullptr, *d_out_off = nullptr;
+    hipError_t e = a.upload(&d_keys, reinterpret_cast<const uint8_t*>(keys.data()), keys.size());
+    if (e == hipSuccess) e = a.upload(&d_offs, key_offs.data(), key_offs.size());
+    if (e == hipSuccess) e = a.upload(&d_first, first.data(), first.size());
+    if (e == hipSuccess) e = a.upload(&d_out_off, out_off.data(), out_off.size());
+    if (e == hipSuccess) e = a.alloc(&d_out, out_total);
+    if (e != hipSuccess) return hip_status(e, "staging");
+    if (lsbm_bloom_build_dev(d_keys, d_offs, internal ? LSBM_INTERNAL_KEY_SUFFIX : 0, d_first,
+                             d_out_off, nf, bpk, d_out, a.stream.get()) != LSBM_OK)
+      return Status::IOError(lsbm_crc32c_last_error());
+    e = a.bounce.to_host(data.data(), d_out, out_total, a.stream.get());
+    if (e != hipSuccess) return hip_status(e, "filters");
+  }
+  for (size_t t = 0; t < n; t++) {  // :41-49
+    std::string& r = results[t];
+    r.assign(data.data() + data_base[t], data_size[t]);
+    for (uint32_t o : offsets[t]) put_fixed32(&r, o);
+    put_fixed32(&r, (uint32_t)data_size[t]);
+    r.push_back((char)LSBM_FILTER_BASE_LG);
+  }
+  return Status::OK();
+}
+
+FilterBlockReader::FilterBlockReader(const BloomOptions& options, const char* contents, size_t n)
+    : options_(options), contents_(contents), size_(n) {}
+
+Status FilterBlockReader::KeyMayMatch(int device, const uint64_t* block_offsets, const char* keys,
+                                      const uint64_t* key_offsets, size_t n,
+                                      std::vector<uint8_t>* may) const {
+  may->assign(n, 1);
+  if (n == 0) return Status::OK();
+  if (!block_offsets || !keys || !key_offsets) return Status::InvalidArgument("null pointer");
+  DeviceArena a;
+  Status s = prepare(device, &a);
+  if (!s.ok()) return s;
+  std::vector<uint64_t> handles(2 * n), offs(n + 1);
+  for (size_t i = 0; i < n; i++) {
+    handles[2 * i] = 0;
+    handles[2 * i + 1] = size_;
+  }
+  for (size_t i = 0; i <= n; i++) offs[i] = key_offsets[i] - key_offsets[0];
+  uint8_t *d_block = nullptr, *d_keys = nullptr, *d_may = nullptr;
+  uint64_t *d_handles = nullptr, *d_data = nullptr, *d_offs = nullptr;
+  hipError_t e = a.upload(&d_block, reinterpret_cast<const uint8_t*>(contents_), size_);
+  if (e == hipSuccess) e = a.upload(&d_handles, handles.data(), handles.size());
+  if (e == hipSuccess) e = a.upload(&d_data, block_offsets, n);
+  if (e == hipSuccess)
+    e = a.upload(&d_keys, reinterpret_cast<const uint8_t*>(keys + key_offsets[0]), offs[n]);
+  if (e == hipSuccess) e = a.upload(&d_offs, offs.data(), offs.size());
+  if (e == hipSuccess) e = a.alloc(&d_may, n);
+  if (e != hipSuccess) return hip_status(e, "staging");
+  if (lsbm_filter_block_may_match_dev(d_block, d_handles, d_data, d_keys, d_offs,
+                                      options_.internal_keys ? LSBM_INTERNAL_KEY_SUFFIX : 0, n,
+                                      options_.bits_per_key, options_.bloom_bits_use, d_may,
+                                      nullptr, a.stream.get()) != LSBM_OK)
+    return Status::IOError(lsbm_crc32c_last_error());
+  e = a.bounce.to_host(may->data(), d_may, n, a.stream.get());
+  return e == hipSuccess ? Status::OK() : hip_status(e, "lookups");
+}
+
+}  // namespace lsbm

@@ -88,6 +88,77 @@ class Oracle:
         return out
 
 
+class BloomOracle:
+    """ctypes view of oracle/liboracle_bloom.so (util/hash.cc, util/bloom.cc,
+    table/filter_block.cc restated in C).  Keys are (uint8 buffer, uint64
+    offsets) pairs, as in tests/golden/bloomkeys.py."""
+
+    def __init__(self, path):
+        lib = ctypes.CDLL(path)
+        u32, u64, vp, sz, i = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_int)
+        lib.bo_hash.restype = u32
+        lib.bo_hash.argtypes = [vp, sz, u32]
+        lib.bo_k_build.restype = sz
+        lib.bo_k_build.argtypes = [i]
+        lib.bo_k_probe.restype = sz
+        lib.bo_k_probe.argtypes = [i, i]
+        lib.bo_filter_bytes.restype = sz
+        lib.bo_filter_bytes.argtypes = [sz, i]
+        lib.bo_create_filter.restype = sz
+        lib.bo_create_filter.argtypes = [vp, vp, sz, i, i, vp]
+        lib.bo_key_may_match.restype = i
+        lib.bo_key_may_match.argtypes = [vp, sz, i, vp, sz, i, i]
+        lib.bo_filter_block_build.restype = sz
+        lib.bo_filter_block_build.argtypes = [vp, vp, i, vp, vp, sz, i, vp, sz]
+        lib.bo_filter_block_may_match.restype = i
+        lib.bo_filter_block_may_match.argtypes = [vp, sz, u64, vp, sz, i, i, i]
+        self.lib = lib
+
+    @staticmethod
+    def _b(x):
+        return np.ascontiguousarray(np.frombuffer(bytes(x), np.uint8) if isinstance(x, (bytes, bytearray)) else x,
+                                    dtype=np.uint8)
+
+    def hash(self, data, seed=0xBC9F1D34):
+        b = self._b(data)
+        return self.lib.bo_hash(b.ctypes.data, b.size, seed & 0xFFFFFFFF)
+
+    def filter_bytes(self, n, bits_per_key):
+        return self.lib.bo_filter_bytes(n, bits_per_key)
+
+    def create_filter(self, keys, bits_per_key, strip=0):
+        b, o = self._b(keys[0]), np.ascontiguousarray(keys[1], dtype=np.uint64)
+        n = o.size - 1
+        out = np.zeros(self.filter_bytes(n, bits_per_key), dtype=np.uint8)
+        self.lib.bo_create_filter(b.ctypes.data, o.ctypes.data, n, strip, bits_per_key,
+                                  out.ctypes.data)
+        return out.tobytes()
+
+    def key_may_match(self, key, filt, bits_per_key, bloom_bits_use=15, strip=0):
+        k, f = self._b(key), self._b(filt)
+        return self.lib.bo_key_may_match(k.ctypes.data, k.size, strip, f.ctypes.data, f.size,
+                                         bits_per_key, bloom_bits_use)
+
+    def filter_block_build(self, keys, block_start, block_first, bits_per_key, strip=0):
+        b, o = self._b(keys[0]), np.ascontiguousarray(keys[1], dtype=np.uint64)
+        st = np.ascontiguousarray(block_start, dtype=np.uint64)
+        fi = np.ascontiguousarray(block_first, dtype=np.uint64)
+        need = self.lib.bo_filter_block_build(b.ctypes.data, o.ctypes.data, strip, st.ctypes.data,
+                                              fi.ctypes.data, st.size, bits_per_key, None, 0)
+        out = np.zeros(need, dtype=np.uint8)
+        self.lib.bo_filter_block_build(b.ctypes.data, o.ctypes.data, strip, st.ctypes.data,
+                                       fi.ctypes.data, st.size, bits_per_key, out.ctypes.data, need)
+        return out.tobytes()
+
+    def filter_block_may_match(self, block, block_offset, key, bits_per_key, bloom_bits_use=15,
+                               strip=0):
+        c, k = self._b(block), self._b(key)
+        return self.lib.bo_filter_block_may_match(c.ctypes.data, c.size, block_offset,
+                                                  k.ctypes.data, k.size, strip, bits_per_key,
+                                                  bloom_bits_use)
+
+
 def _build(target_dir, artefact):
     path = os.path.join(REPO, target_dir, artefact)
     if not os.path.exists(path):
@@ -99,6 +170,17 @@ def _build(target_dir, artefact):
 @pytest.fixture(scope="session")
 def oracle():
     return Oracle(_build("oracle", "liboracle_crc32c.so"))
+
+
+@pytest.fixture(scope="session")
+def bloom_oracle():
+    return BloomOracle(_build("oracle", "liboracle_bloom.so"))
+
+
+@pytest.fixture(scope="session")
+def bloom_golden():
+    with open(os.path.join(TESTS, "golden", "bloom_fixture.json")) as f:
+        return json.load(f)
 
 
 @pytest.fixture(scope="session")

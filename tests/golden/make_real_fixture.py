@@ -11,7 +11,11 @@ dir, then extracts
     TableBuilder::WriteRawBlock wrote them (table/table_builder.cc:237-255);
   * from the WAL: the first 200 physical records [crc 4][len 2][type 1][payload]
     as log::Writer::EmitPhysicalRecord wrote them (common/log_writer.cc:75-100).
-Writes tests/golden/real_sst.bin, real_wal.bin and real_fixture.json.  Only
+  * the table's filter block (table/filter_block.cc format, written by
+    InternalFilterPolicy over BloomFilterPolicy(20)): its filters up to the one
+    that covers the last of those 96 data blocks, and the whole offset array.
+Writes tests/golden/real_sst.bin, real_wal.bin, real_filter.bin and
+real_fixture.json.  Only
 bytes produced by the reference are stored; no reference source.
 """
 import json
@@ -90,6 +94,21 @@ def main():
                          "stored_masked_crc": struct.unpack_from("<I", region, size + 1)[0],
                          "file_offset": off})
         sst_bin += region
+    meta_block = tab[meta_h[0]:meta_h[0] + meta_h[1]]
+    filt = None
+    for k, v in block_entries(meta_block):
+        if k == b"filter.leveldb.BuiltinBloomFilter":  # table/table_builder.cc:280-284
+            fh = handle(v, 0)[0]
+            fb = tab[fh[0]:fh[0] + fh[1]]
+            array_offset = struct.unpack_from("<I", fb, len(fb) - 5)[0]
+            n_f = (len(fb) - 5 - array_offset) // 4
+            offsets = list(struct.unpack_from("<%dI" % n_f, fb, array_offset))
+            last = picked[95][1] if len(data_handles) > 95 else picked[-3][1]
+            covered = (last[0] + last[1] + 5) // 2048  # filters complete after that block
+            end = offsets[covered] if covered < n_f else array_offset
+            filt = {"handle": list(fh), "base_lg": fb[-1], "array_offset": array_offset,
+                    "offsets": offsets, "prefix_bytes": end}
+            open(os.path.join(HERE, "real_filter.bin"), "wb").write(fb[:end])
     wal = open(os.path.join(d, logs[0]), "rb").read()
     wal_bin, wal_meta, pos = bytearray(), [], 0
     while len(wal_meta) < 200 and pos + 7 <= len(wal):
@@ -110,7 +129,7 @@ def main():
     json.dump({"source": "lsbm db_bench built from /root/reference (oracle/Makefile dbbench); "
                          + " ".join(os.path.basename(a) if i == 0 else a
                                     for i, a in enumerate(args) if not a.startswith("--db=")),
-               "table_file": tables[0], "table_blocks": sst_meta,
+               "table_file": tables[0], "table_blocks": sst_meta, "filter": filt,
                "wal_file": logs[0], "wal_records": wal_meta},
               open(os.path.join(HERE, "real_fixture.json"), "w"), indent=0)
     print(f"{len(sst_meta)} table blocks ({len(sst_bin)} B), {len(wal_meta)} WAL records "

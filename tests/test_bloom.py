@@ -1,0 +1,477 @@
+"""SSTable bloom filters (util/hash.cc, util/bloom.cc, table/filter_block.cc).
+
+Parity is pinned by tests/golden/bloom_fixture.json, which the reference's
+own Hash / BloomFilterPolicy / FilterBlockBuilder / FilterBlockReader produced
+(tests/golden/make_bloom_fixture.py), and by the filter block of a real
+db_bench SSTable (tests/golden/real_filter.bin, tests/golden/make_real_fixture.py).
+CPU tests: the oracle (oracle/bloom_oracle.c) against both, and the product's
+host API.  GPU tests: every batch entry point of include/lsbm_bloom.h and the
+C++ layer include/lsbm/filter_block.h against the oracle and the fixtures.
+"""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden.bloomkeys import concat, dbbench_keys, random_keys, take
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+G = os.path.join(HERE, "golden")
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def key_at(keys, i):
+    b, o = keys
+    return b[int(o[i]):int(o[i + 1])].tobytes()
+
+
+def make_keys(spec):
+    if spec["kind"] == "dbbench":
+        return dbbench_keys(spec["first"], spec["n"])
+    return random_keys(spec["seed"], spec["n"], spec["lo"], spec["hi"])
+
+
+def apply(img, ops):
+    img = bytearray(img)
+    for op in ops:
+        if op[0] == "set":
+            b = bytes.fromhex(op[2])
+            img[op[1]:op[1] + len(b)] = b
+        elif op[0] == "truncate":
+            img = img[:op[1]]
+    return bytes(img)
+
+
+def block_queries(bx):
+    """(keys, block offsets) of a fixture block scenario's lookups."""
+    keys = make_keys(bx["keys"])
+    nk, strip = bx["keys"]["n"], bx["strip"]
+    q = [key_at(keys, i) for i in range(nk)]
+    others = random_keys(bx["queries"]["others_seed"], 64, 1, 30)
+    q += [key_at(others, i) + bytes(strip) for i in range(64)]
+    q += [key_at(keys, 0) if nk else b"x" * (strip + 1)] * 4
+    lens = np.array([len(x) for x in q], dtype=np.uint64)
+    offs = np.zeros(len(q) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    buf = np.frombuffer(b"".join(q), dtype=np.uint8).copy()
+    return (buf, offs), np.array(bx["queries"]["offsets"], dtype=np.uint64)
+
+
+@pytest.fixture(scope="module")
+def real_filter():
+    meta = json.load(open(os.path.join(G, "real_fixture.json")))
+    if "filter" not in meta:
+        pytest.skip("real fixture has no filter block")
+    blob = np.fromfile(os.path.join(G, "real_filter.bin"), dtype=np.uint8)
+    sst = np.fromfile(os.path.join(G, "real_sst.bin"), dtype=np.uint8)
+    return meta, blob, sst
+
+
+def real_table_keys(meta, sst):
+    """Internal keys of the fixture's data blocks (table/block.cc format) and
+    the StartBlock/AddKey sequence TableBuilder made for them."""
+    import struct
+
+    def varint(b, p):
+        r, s = 0, 0
+        while True:
+            c = b[p]
+            p += 1
+            r |= (c & 0x7F) << s
+            if c < 0x80:
+                return r, p
+            s += 7
+
+    keys, starts, first = [], [], [0]
+    for b in meta["table_blocks"]:
+        if b["kind"] != "data":
+            continue
+        blk = sst[b["offset"]:b["offset"] + b["size"]].tobytes()
+        nrest = struct.unpack_from("<I", blk, len(blk) - 4)[0]
+        limit, p, key = len(blk) - 4 - 4 * nrest, 0, b""
+        while p < limit:
+            sh, p = varint(blk, p)
+            ns, p = varint(blk, p)
+            vl, p = varint(blk, p)
+            key = key[:sh] + blk[p:p + ns]
+            p += ns + vl
+            keys.append(key)
+        starts.append(b["file_offset"])
+        first.append(len(keys))
+    last = [b for b in meta["table_blocks"] if b["kind"] == "data"][-1]
+    starts.append(last["file_offset"] + last["size"] + 5)  # StartBlock after the last block
+    first.append(len(keys))
+    lens = np.array([len(k) for k in keys], dtype=np.uint64)
+    offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    return (np.frombuffer(b"".join(keys), np.uint8).copy(), offs), starts, first
+
+
+# ---------------------------------------------------------------- CPU: oracle pinned
+def test_oracle_hash_matches_reference(bloom_oracle, bloom_golden):
+    h = bloom_golden["hash"]
+    keys = random_keys(h["keys"]["seed"], h["keys"]["n"], h["keys"]["lo"], h["keys"]["hi"])
+    for seed, vals in h["values"].items():
+        got = [bloom_oracle.hash(key_at(keys, i), int(seed)) for i in range(len(vals))]
+        assert got == vals, seed
+
+
+def test_oracle_create_filter_matches_reference(bloom_oracle, bloom_golden):
+    for c in bloom_golden["create"]:
+        keys = random_keys(c["seed"], c["n"], c["lo"], c["hi"])
+        f = bloom_oracle.create_filter(keys, c["bits_per_key"])
+        assert len(f) == c["len"] and sha(f) == c["sha256"], (c["bits_per_key"], c["n"])
+
+
+def test_oracle_key_may_match_matches_reference(bloom_oracle, bloom_golden):
+    for p in bloom_golden["probe"]:
+        members = random_keys(p["members"]["seed"], p["members"]["n"], 1, 30, printable=True)
+        others = random_keys(p["others"]["seed"], p["others"]["n"], 1, 30, printable=True)
+        filt = bloom_oracle.create_filter(members, p["bits_per_key"])
+        assert sha(filt) == p["filter"]["sha256"]
+        probes = concat(members, others)
+        got = "".join(str(bloom_oracle.key_may_match(key_at(probes, i), filt, p["bits_per_key"],
+                                                     p["bloom_bits_use"]))
+                      for i in range(len(p["may"])))
+        assert got == p["may"], (p["bits_per_key"], p["bloom_bits_use"])
+        assert got[:p["members"]["n"]] == "1" * p["members"]["n"]  # no false negatives
+    for e in bloom_golden["probe_edge"]:
+        keys = random_keys(e["keys"]["seed"], e["keys"]["n"], e["keys"]["lo"], e["keys"]["hi"])
+        f = bytes.fromhex(e["filter_hex"])
+        got = "".join(str(bloom_oracle.key_may_match(key_at(keys, i), f, e["bits_per_key"]))
+                      for i in range(e["keys"]["n"]))
+        assert got == e["may"], e["name"]
+
+
+def test_oracle_filter_blocks_match_reference(bloom_oracle, bloom_golden):
+    for bx in bloom_golden["blocks"]:
+        keys = make_keys(bx["keys"])
+        block = bloom_oracle.filter_block_build(keys, bx["block_start"], bx["block_first"],
+                                                bx["bits_per_key"], bx["strip"])
+        assert len(block) == bx["block"]["len"] and sha(block) == bx["block"]["sha256"], bx["name"]
+        qk, qo = block_queries(bx)
+        for sc in bx["lookups"]:
+            img = apply(block, sc["ops"])
+            got = "".join(str(bloom_oracle.filter_block_may_match(
+                img, int(qo[j]), key_at(qk, j), bx["bits_per_key"], 15, bx["strip"]))
+                for j in range(qo.size))
+            assert got == sc["may"], (bx["name"], sc["name"])
+
+
+def test_oracle_rebuilds_real_sstable_filters(bloom_oracle, real_filter):
+    """The filters lsbm's db_bench wrote for the fixture's 96 data blocks
+    (InternalFilterPolicy over BloomFilterPolicy(20), table/table_builder.cc)."""
+    meta, blob, sst = real_filter
+    keys, starts, first = real_table_keys(meta, sst)
+    block = np.frombuffer(bloom_oracle.filter_block_build(keys, starts, first, 20, strip=8),
+                          np.uint8)
+    fm = meta["filter"]
+    # our block covers the first filters of the real one: same filter bytes, same offsets
+    n_ours = (block.size - 5 - int.from_bytes(block[-5:-1].tobytes(), "little")) // 4
+    ours_offs = np.frombuffer(block[block.size - 5 - 4 * n_ours:block.size - 5].tobytes(), "<u4")
+    assert n_ours <= len(fm["offsets"])
+    assert ours_offs.tolist() == fm["offsets"][:n_ours]
+    data_len = int.from_bytes(block[-5:-1].tobytes(), "little")  # our array_offset
+    assert data_len == fm["prefix_bytes"] == blob.size
+    assert np.array_equal(block[:data_len], blob)
+    # every key of those blocks may match at its block (no false negatives)
+    for b in range(len(starts) - 1):
+        for k in range(first[b], first[b + 1], 7):
+            assert bloom_oracle.filter_block_may_match(blob, starts[b], key_at(keys, k), 20, 15, 8)
+
+
+# ---------------------------------------------------------------- CPU: product host API
+def test_host_hash_and_sizes(product_lib, bloom_golden, bloom_oracle):
+    from lsbm_amd import bloom
+    h = bloom_golden["hash"]
+    keys = random_keys(h["keys"]["seed"], h["keys"]["n"], h["keys"]["lo"], h["keys"]["hi"])
+    for seed, vals in h["values"].items():
+        assert [bloom.hash(key_at(keys, i), int(seed)) for i in range(len(vals))] == vals
+    for bpk in [-1, 0, 1, 10, 20, 45, 100]:
+        for bbu in [-3, 0, 3, 15, 200]:
+            if bpk >= 0:
+                assert bloom.k_probe(bpk, bbu) == bloom_oracle.lib.bo_k_probe(bpk, bbu)
+        if bpk >= 0:
+            assert bloom.k_build(bpk) == bloom_oracle.lib.bo_k_build(bpk)
+            for n in [0, 1, 3, 4, 33, 1000]:
+                assert bloom.filter_bytes(n, bpk) == bloom_oracle.filter_bytes(n, bpk)
+        else:
+            assert bloom.filter_bytes(3, bpk) == 0
+
+
+def test_python_layout_matches_oracle_block(bloom_oracle, bloom_golden):
+    """lsbm_amd.bloom.layout_filter_block reproduces FilterBlockBuilder's
+    layout (offset array, array_offset, base_lg) for every fixture scenario."""
+    from lsbm_amd import bloom
+    for bx in bloom_golden["blocks"]:
+        keys = make_keys(bx["keys"])
+        lay = bloom.layout_filter_block(bx["block_start"], bx["block_first"], bx["bits_per_key"])
+        ref = bloom_oracle.filter_block_build(keys, bx["block_start"], bx["block_first"],
+                                              bx["bits_per_key"], bx["strip"])
+        assert lay.total_bytes == len(ref), bx["name"]
+        assert ref[lay.data_bytes:] == lay.trailer, bx["name"]
+        # filters: the oracle's bytes of each non-empty filter
+        for (k0, k1), off in zip(lay.filter_keys, lay.filter_out):
+            f = bloom_oracle.create_filter(take(keys, range(k0, k1)), bx["bits_per_key"],
+                                           bx["strip"])
+            assert ref[off:off + len(f)] == f
+
+
+def test_cpp_hash_links_unchanged(product_lib, tmp_path):
+    """util/hash.h's leveldb::Hash resolves to the library's exported symbol."""
+    src = tmp_path / "hash_link.cc"
+    src.write_text('#include "util/hash.h"\n#include <stdio.h>\n'
+                   'int main(){ unsigned h = leveldb::Hash("hello", 5, 0xbc9f1d34);'
+                   ' printf("%08x\\n", h); return 0; }\n')
+    exe = tmp_path / "hash_link"
+    libdir = os.path.join(REPO, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-I", os.path.join(REPO, "include"), str(src), "-L", libdir,
+                    "-llsbm_crc32c", "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.strip()
+    from conftest import BloomOracle
+    o = BloomOracle(os.path.join(REPO, "oracle", "liboracle_bloom.so"))
+    assert int(out, 16) == o.hash(b"hello")
+
+
+def test_bloom_entry_points_fail_loudly_without_device(product_lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from lsbm_amd import _lib
+    L = _lib.lib()
+    z = np.zeros(16, dtype=np.uint64)
+    out = np.zeros(64, dtype=np.uint8)
+    rc = L.lsbm_bloom_build_dev(out.ctypes.data, z.ctypes.data, 0, z.ctypes.data, z.ctypes.data,
+                                1, 10, out.ctypes.data, None)
+    assert rc == _lib.LSBM_ERR_NO_DEVICE
+    assert L.lsbm_bloom_build_dev(None, None, 0, None, None, 1, 10, None, None) == \
+        _lib.LSBM_ERR_INVALID
+    assert L.lsbm_bloom_build_dev(None, None, 0, None, None, 0, 10, None, None) == _lib.LSBM_OK
+
+
+# ---------------------------------------------------------------- GPU
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def _i64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)
+
+
+def gpu_build(torch, keys, filters, bits_per_key, strip=0, gap=0):
+    """Build the filters [(k0, k1), ...] of `keys` on the GPU, laid out back
+    to back (plus `gap` spare bytes between them).  Returns (out bytes,
+    offsets)."""
+    from lsbm_amd import bloom
+    first = np.array([f[0] for f in filters] + [filters[-1][1]], dtype=np.uint64)
+    sizes = [bloom.filter_bytes(k1 - k0, bits_per_key) for k0, k1 in filters]
+    offs = np.zeros(len(filters), dtype=np.uint64)
+    pos = 0
+    for i, s in enumerate(sizes):
+        pos += gap
+        offs[i] = pos
+        pos += s
+    total = pos + gap
+    out = torch.full((total + 8,), 0xEE, dtype=torch.uint8, device="cuda")
+    kb = keys[0] if keys[0].size else np.zeros(1, np.uint8)  # a device pointer even with no keys
+    bloom.build_filters(_dev(torch, kb), _dev(torch, _i64(keys[1])),
+                        _dev(torch, _i64(first)), _dev(torch, _i64(offs)), out, bits_per_key,
+                        strip=strip)
+    return out.cpu().numpy(), offs, sizes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits_per_key", [0, 1, 3, 10, 20, 45])
+@pytest.mark.parametrize("strip,gap", [(0, 0), (8, 3)])
+def test_gpu_build_matches_oracle(torch_cuda, bloom_oracle, bits_per_key, strip, gap):
+    torch = torch_cuda
+    rng = np.random.default_rng(bits_per_key * 7 + strip)
+    counts = rng.integers(0, 80, size=400)
+    counts[::50] = rng.integers(300, 3000, size=counts[::50].size)  # multi-window filters
+    counts[5] = 0
+    n = int(counts.sum())
+    keys = random_keys(1000 + bits_per_key, n, strip, strip + 40)
+    filters, k = [], 0
+    for c in counts:
+        filters.append((k, k + int(c)))
+        k += int(c)
+    out, offs, sizes = gpu_build(torch, keys, filters, bits_per_key, strip, gap)
+    for i, (k0, k1) in enumerate(filters):
+        want = bloom_oracle.create_filter(take(keys, range(k0, k1)), bits_per_key, strip)
+        got = out[int(offs[i]):int(offs[i]) + sizes[i]].tobytes()
+        assert got == want, i
+    if gap:  # bytes between filters are untouched
+        for i in range(len(filters)):
+            assert np.all(out[int(offs[i]) - gap:int(offs[i])] == 0xEE)
+
+
+@pytest.mark.gpu
+def test_gpu_build_reference_vectors(torch_cuda, bloom_golden):
+    torch = torch_cuda
+    for c in bloom_golden["create"]:
+        keys = random_keys(c["seed"], c["n"], c["lo"], c["hi"])
+        out, offs, sizes = gpu_build(torch, keys, [(0, c["n"])], c["bits_per_key"])
+        assert sha(out[:sizes[0]]) == c["sha256"], (c["bits_per_key"], c["n"])
+
+
+@pytest.mark.gpu
+def test_gpu_filter_block_reference_vectors(torch_cuda, bloom_golden, bloom_oracle):
+    """Python FilterBlockBuilder mirror: layout on the host, every filter in
+    one GPU launch; equals the reference's FilterBlockBuilder output."""
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    for bx in bloom_golden["blocks"]:
+        keys = make_keys(bx["keys"])
+        block = bloom.build_filter_block(_dev(torch, keys[0]), _dev(torch, _i64(keys[1])),
+                                         bx["block_start"], bx["block_first"],
+                                         bx["bits_per_key"], strip=bx["strip"])
+        assert sha(block) == bx["block"]["sha256"], bx["name"]
+
+
+@pytest.mark.gpu
+def test_gpu_may_match_reference_vectors(torch_cuda, bloom_golden, bloom_oracle):
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    for p in bloom_golden["probe"]:
+        members = random_keys(p["members"]["seed"], p["members"]["n"], 1, 30, printable=True)
+        others = random_keys(p["others"]["seed"], p["others"]["n"], 1, 30, printable=True)
+        filt = np.frombuffer(bloom_oracle.create_filter(members, p["bits_per_key"]), np.uint8)
+        probes = concat(members, others)
+        nq = probes[1].size - 1
+        handles = np.tile(np.array([0, filt.size], dtype=np.int64), nq)
+        may, n_may = bloom.may_match(_dev(torch, filt), _dev(torch, handles),
+                                     _dev(torch, probes[0]), _dev(torch, _i64(probes[1])),
+                                     p["bits_per_key"], p["bloom_bits_use"])
+        got = "".join(str(int(x)) for x in may.cpu().numpy())
+        assert got == p["may"] and int(n_may.item()) == got.count("1")
+    for e in bloom_golden["probe_edge"]:
+        keys = random_keys(e["keys"]["seed"], e["keys"]["n"], e["keys"]["lo"], e["keys"]["hi"])
+        f = np.frombuffer(bytes.fromhex(e["filter_hex"]) + b"\0", np.uint8)  # +1: non-empty tensor
+        handles = np.tile(np.array([0, f.size - 1], dtype=np.int64), e["keys"]["n"])
+        may, _ = bloom.may_match(_dev(torch, f), _dev(torch, handles), _dev(torch, keys[0]),
+                                 _dev(torch, _i64(keys[1])), e["bits_per_key"])
+        assert "".join(str(int(x)) for x in may.cpu().numpy()) == e["may"], e["name"]
+
+
+@pytest.mark.gpu
+def test_gpu_filter_block_lookups_reference_vectors(torch_cuda, bloom_golden, bloom_oracle):
+    """FilterBlockReader::KeyMayMatch on every fixture block, as built and
+    corrupted, in one launch per scenario."""
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    for bx in bloom_golden["blocks"]:
+        keys = make_keys(bx["keys"])
+        block = bloom_oracle.filter_block_build(keys, bx["block_start"], bx["block_first"],
+                                                bx["bits_per_key"], bx["strip"])
+        qk, qo = block_queries(bx)
+        nq = qo.size
+        for sc in bx["lookups"]:
+            img = np.frombuffer(apply(block, sc["ops"]) + b"\0", np.uint8)
+            handles = np.tile(np.array([0, img.size - 1], dtype=np.int64), nq)
+            may, n_may = bloom.filter_block_may_match(
+                _dev(torch, img), _dev(torch, handles), _dev(torch, _i64(qo)),
+                _dev(torch, qk[0]), _dev(torch, _i64(qk[1])), bx["bits_per_key"],
+                strip=bx["strip"])
+            got = "".join(str(int(x)) for x in may.cpu().numpy())
+            assert got == sc["may"], (bx["name"], sc["name"])
+            assert int(n_may.item()) == got.count("1")
+
+
+@pytest.mark.gpu
+def test_gpu_real_sstable_filters(torch_cuda, real_filter, bloom_oracle):
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    meta, blob, sst = real_filter
+    keys, starts, first = real_table_keys(meta, sst)
+    block = np.frombuffer(bloom.build_filter_block(_dev(torch, keys[0]), _dev(torch, _i64(keys[1])),
+                                                   starts, first, 20, strip=8), np.uint8)
+    assert block.tobytes() == bloom_oracle.filter_block_build(keys, starts, first, 20, strip=8)
+    data_len = int.from_bytes(block[-5:-1].tobytes(), "little")  # our array_offset
+    assert data_len == blob.size and np.array_equal(block[:data_len], blob)
+    # all member keys against the REAL filter block: no false negatives
+    nk = keys[1].size - 1
+    offs = np.zeros(nk, dtype=np.uint64)
+    for b in range(len(starts) - 1):
+        offs[first[b]:first[b + 1]] = starts[b]
+    handles = np.tile(np.array([0, blob.size], dtype=np.int64), nk)
+    may, n_may = bloom.filter_block_may_match(_dev(torch, blob), _dev(torch, handles),
+                                              _dev(torch, _i64(offs)), _dev(torch, keys[0]),
+                                              _dev(torch, _i64(keys[1])), 20, strip=8)
+    assert int(n_may.item()) == nk and bool(may.all())
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_no_false_negatives(torch_cuda, bloom_oracle):
+    """db_bench-shaped batch at scale (2M internal keys, 33 per filter):
+    every member probes 1, sampled filters equal the oracle's, non-member
+    results equal the oracle's on a sample."""
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    n, per = 1 << 21, 33
+    keys = dbbench_keys(0, n)
+    filters = [(k, min(n, k + per)) for k in range(0, n, per)]
+    out, offs, sizes = gpu_build(torch, keys, filters, 20, strip=8)
+    rng = np.random.default_rng(5)
+    for i in rng.choice(len(filters), 40, replace=False):
+        k0, k1 = filters[i]
+        assert out[int(offs[i]):int(offs[i]) + sizes[i]].tobytes() == \
+            bloom_oracle.create_filter(take(keys, range(k0, k1)), 20, 8)
+    fidx = np.arange(n) // per
+    handles = np.stack([offs[fidx].astype(np.int64), np.array(sizes, np.int64)[fidx]], 1).reshape(-1)
+    dout = _dev(torch, out)
+    may, n_may = bloom.may_match(dout, _dev(torch, handles), _dev(torch, keys[0]),
+                                 _dev(torch, _i64(keys[1])), 20, strip=8)
+    assert int(n_may.item()) == n
+    miss = dbbench_keys(n, n)  # never inserted
+    may2, n2 = bloom.may_match(dout, _dev(torch, handles), _dev(torch, miss[0]),
+                               _dev(torch, _i64(miss[1])), 20, strip=8)
+    m2 = may2.cpu().numpy()
+    for q in rng.choice(n, 300, replace=False):
+        f = int(fidx[q])
+        filt = out[int(offs[f]):int(offs[f]) + sizes[f]].tobytes()
+        assert m2[q] == bloom_oracle.key_may_match(key_at(miss, q), filt, 20, 15, 8)
+    assert 0 < int(n2.item()) < n // 50  # ~0.1-0.5% false positives at 20 bits/key, k_use 10
+
+
+@pytest.mark.gpu
+def test_cpp_filter_block_layer(torch_cuda, bloom_golden, tmp_path, bloom_oracle, real_filter):
+    """include/lsbm/filter_block.h: FilterBlockBuilder / FinishFilterBlocks /
+    FilterBlockReader, driven by tests/cpp/filter_tool.cc."""
+    exe = tmp_path / "filter_tool"
+    libdir = os.path.join(REPO, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+                    os.path.join(HERE, "cpp", "filter_tool.cc"), "-L", libdir, "-llsbm_crc32c",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    meta, blob, sst = real_filter
+    cases = [(make_keys(bx["keys"]), bx["block_start"], bx["block_first"], bx["bits_per_key"],
+              bx["strip"], bx["block"]["sha256"]) for bx in bloom_golden["blocks"]]
+    keys, starts, first = real_table_keys(meta, sst)
+    cases.append((keys, starts, first, 20, 8, sha(bloom_oracle.filter_block_build(
+        keys, starts, first, 20, 8))))
+    for ci, (keys, starts, first, bpk, strip, want) in enumerate(cases):
+        kf, of, bf, out = (tmp_path / f"k{ci}", tmp_path / f"o{ci}", tmp_path / f"b{ci}",
+                           tmp_path / f"out{ci}")
+        keys[0].tofile(kf)
+        keys[1].astype("<u8").tofile(of)
+        np.concatenate([[len(starts)], starts, first]).astype("<u8").tofile(bf)
+        subprocess.run([str(exe), "build", str(kf), str(of), str(bf), str(out), str(bpk),
+                        str(strip), "3"], check=True, timeout=120)
+        block = np.fromfile(out, dtype=np.uint8).tobytes()
+        assert sha(block) == want, ci
+        # reader: every member at its block, batched
+        nk = keys[1].size - 1
+        qo = np.zeros(nk, dtype=np.uint64)
+        for b in range(len(starts)):
+            qo[first[b]:first[b + 1]] = starts[b]
+        qf = tmp_path / f"q{ci}"
+        qo.astype("<u8").tofile(qf)
+        r = subprocess.run([str(exe), "probe", str(out), str(kf), str(of), str(qf), str(bpk), "15",
+                            str(strip)], check=True, capture_output=True, text=True, timeout=120)
+        assert r.stdout.strip() == "1" * nk, ci

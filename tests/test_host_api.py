@@ -20,9 +20,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    text = open(os.path.join(REPO, "include", "lsbm_crc32c.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(lsbm_\w+)\s*\(", text)))
+    """Every C function the C-ABI headers (include/lsbm_*.h) declare."""
+    names = set()
+    for h in ("lsbm_crc32c.h", "lsbm_bloom.h"):
+        text = open(os.path.join(REPO, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names |= set(re.findall(r"\b(lsbm_\w+)\s*\(", text))
+    return sorted(names)
 
 
 def test_exports_every_declared_symbol(product_lib):
@@ -34,6 +38,7 @@ def test_exports_every_declared_symbol(product_lib):
     missing = [n for n in names if n not in exported]
     assert not missing, missing
     assert "_ZN7leveldb6crc32c6ExtendEjPKcm" in exported  # util/crc32c.h:17
+    assert "_ZN7leveldb4HashEPKcmj" in exported  # util/hash.h:15
     from lsbm_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
 
