@@ -58,19 +58,25 @@ def build_filters(keys, key_offsets, filter_first, filter_out, out, bits_per_key
     return out
 
 
-def _probe_out(n, device):
+def _probe_out(n, device, may, n_may):
+    """Result tensors: given ones are reused (n_may accumulates), else new."""
     torch = _torch()
-    return (torch.empty(n, dtype=torch.uint8, device=device),
-            torch.zeros(1, dtype=torch.int32, device=device))
+    if may is None:
+        may = torch.empty(n, dtype=torch.uint8, device=device)
+    if n_may is None:
+        n_may = torch.zeros(1, dtype=torch.int32, device=device)
+    if may.numel() < n:
+        raise ValueError("may needs one byte per query")
+    return may, n_may
 
 
 def may_match(filters, handles, keys, key_offsets, bits_per_key, bloom_bits_use=15, strip=0,
-              stream=None):
+              stream=None, may=None, n_may=None):
     """Query q: key q against filters[handles[2q], + handles[2q+1]).
-    Returns (may uint8[n], n_may int32[1])."""
+    Returns (may uint8[n], n_may int32[1]); the count is added to a given n_may."""
     _require_cuda(filters, handles, keys, key_offsets)
     n = key_offsets.numel() - 1
-    may, n_may = _probe_out(n, filters.device)
+    may, n_may = _probe_out(n, filters.device, may, n_may)
     check(lib().lsbm_bloom_may_match_dev(_ptr(filters), _ptr(handles), _ptr(keys),
                                          _ptr(key_offsets), strip, n, bits_per_key,
                                          bloom_bits_use, _ptr(may), _ptr(n_may),
@@ -79,12 +85,12 @@ def may_match(filters, handles, keys, key_offsets, bits_per_key, bloom_bits_use=
 
 
 def filter_block_may_match(blocks, handles, data_offsets, keys, key_offsets, bits_per_key,
-                           bloom_bits_use=15, strip=0, stream=None):
+                           bloom_bits_use=15, strip=0, stream=None, may=None, n_may=None):
     """Query q: FilterBlockReader(blocks[handles[2q], + handles[2q+1]])
     .KeyMayMatch(data_offsets[q], key q).  Returns (may, n_may)."""
     _require_cuda(blocks, handles, data_offsets, keys, key_offsets)
     n = key_offsets.numel() - 1
-    may, n_may = _probe_out(n, blocks.device)
+    may, n_may = _probe_out(n, blocks.device, may, n_may)
     check(lib().lsbm_filter_block_may_match_dev(_ptr(blocks), _ptr(handles), _ptr(data_offsets),
                                                 _ptr(keys), _ptr(key_offsets), strip, n,
                                                 bits_per_key, bloom_bits_use, _ptr(may),

@@ -81,8 +81,9 @@ __attribute__((visibility("default"))) int lsbm_bloom_build_dev(
   a.bits_per_key = (uint64_t)bits_per_key;
   a.strip = strip;
   a.k = lsbm_bloom_k(bits_per_key);
-  // one wave per filter; 8 workgroups of 4 waves per CU (LDS: 16 KiB each)
-  const hipError_t e = launch_bloom_build(a, grid_for(cus, n_filters, kBloomWaves, 8),
+  // one wave per group of kBloomGroup filters; up to 8 workgroups of 4 waves per CU
+  const uint64_t groups = (n_filters + kBloomGroup - 1) / kBloomGroup;
+  const hipError_t e = launch_bloom_build(a, grid_for(cus, groups, kBloomWaves, 8),
                                           static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_build_kernel");
 }

@@ -45,7 +45,7 @@ __device__ uint32_t hash_key(uint64_t s, uint64_t n, uint32_t seed) {
   const uint32_t sh = (uint32_t)s & 3u;
   uint64_t q = s & ~3ull;
   uint32_t lo = *reinterpret_cast<gcu32>(q);
-  for (uint64_t k = n >> 2; k; k--) {
+  for (uint64_t k = n >> 2; k; k--) {  // 4-byte steps (:26-32)
     q += 4;
     const uint32_t hi = *reinterpret_cast<gcu32>(q < w_last ? q : w_last);
     h += __builtin_amdgcn_alignbyte(hi, lo, sh);
@@ -54,7 +54,7 @@ __device__ uint32_t hash_key(uint64_t s, uint64_t n, uint32_t seed) {
     lo = hi;
   }
   const uint32_t r = (uint32_t)n & 3u;
-  if (r) {
+  if (r) {  // the byte tail (:35-47)
     q += 4;
     const uint32_t hi = *reinterpret_cast<gcu32>(q < w_last ? q : w_last);
     const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
@@ -63,6 +63,45 @@ __device__ uint32_t hash_key(uint64_t s, uint64_t n, uint32_t seed) {
     h += sext8(w);
     h *= kHashM;
     h ^= h >> 24;
+  }
+  return h;
+}
+
+// The same hash for latency-bound callers (the probe kernel): the words of up
+// to 8 steps (32 key bytes) are all requested before the first is used, so a
+// key costs one memory round trip per 32 bytes instead of one per 4 (a
+// db_bench user key, 23 B, is one round trip).  More VALU than hash_key.
+__device__ uint32_t hash_key_batched(uint64_t s, uint64_t n, uint32_t seed) {
+  uint32_t h = seed ^ (uint32_t)(n * kHashM);
+  if (n == 0) return h;
+  const uint64_t w0 = s & ~3ull, w_last = (s + n - 1) & ~3ull;
+  const uint32_t sh = (uint32_t)s & 3u;
+  const uint64_t full = n >> 2;
+  const uint32_t r = (uint32_t)n & 3u;
+  const uint64_t steps = full + (r ? 1 : 0);
+  for (uint64_t c = 0; c < steps; c += 8) {
+    uint32_t w[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const uint64_t q = w0 + 4 * (c + j);
+      w[j] = *reinterpret_cast<gcu32>(q < w_last ? q : w_last);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = c + j;
+      const uint32_t x = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+      if (t < full) {
+        h += x;
+        h *= kHashM;
+        h ^= h >> 16;
+      } else if (t == full && r) {
+        if (r == 3) h += sext8(x >> 16) << 16;
+        if (r >= 2) h += sext8(x >> 8) << 8;
+        h += sext8(x);
+        h *= kHashM;
+        h ^= h >> 24;
+      }
+    }
   }
   return h;
 }
@@ -103,6 +142,16 @@ __device__ __forceinline__ uint32_t mod_bits(uint32_t h, const BitMod& m) {
   return (uint32_t)r;
 }
 
+// n % d for 32-bit n and d by one 64-bit multiply-high chain, with
+// M = ceil(2^64 / d) computed once per filter (Lemire, Kaser & Kurz, "Faster
+// remainder by direct computation", 2019: exact for every 32-bit n and d).
+__device__ __forceinline__ uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
+__device__ __forceinline__ uint32_t fastmod(uint32_t n, uint64_t M, uint32_t d) {
+  const uint64_t low = M * n;  // mod 2^64
+  const uint64_t lo = (uint64_t)(uint32_t)low * d, hi = (low >> 32) * d;
+  return (uint32_t)((hi + (lo >> 32)) >> 32);  // high 64 bits of low * d
+}
+
 // Orders one wave's LDS phases (its own ds ops complete in order; this keeps
 // the compiler from moving accesses across the phase boundary).
 __device__ __forceinline__ void wave_phase() {
@@ -128,44 +177,134 @@ __device__ __forceinline__ void store_window(uint64_t d, const uint32_t* bm, uin
     *reinterpret_cast<gu32>(d + head + 4ull * i) = __builtin_amdgcn_alignbyte(bm[i + 1], bm[i], head);
 }
 
+// One filter, keys [k0, k1), written to out + fo, in LDS windows of
+// kBloomWindowBytes (the path for filters a packed batch cannot hold).
+__device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uint64_t fo,
+                          uint32_t* bm, uint32_t lane) {
+  // util/bloom.cc:39-46: bits = max(64, n * bits_per_key), rounded up to bytes
+  const uint64_t nk = k1 > k0 ? k1 - k0 : 0;
+  uint64_t bits = nk * a.bits_per_key;
+  if (bits < 64) bits = 64;
+  const uint64_t bytes = (bits + 7) / 8;
+  const BitMod m = bit_mod(bytes * 8);
+  const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + fo;
+  for (uint64_t win = 0; win < bytes; win += kBloomWindowBytes) {
+    const uint32_t wbytes =
+        (uint32_t)(bytes - win < kBloomWindowBytes ? bytes - win : kBloomWindowBytes);
+    const uint64_t bit0 = win * 8, nbits = (uint64_t)wbytes * 8;
+    for (uint32_t i = lane; i <= wbytes / 4; i += 64) bm[i] = 0;  // + 1 pad word
+    wave_phase();
+    // util/bloom.cc:52-62: double hashing, delta = h rotated right 17
+    for (uint64_t i = k0 + lane; i < k1; i += 64) {
+      uint64_t s, n;
+      key_extent(a.keys, a.key_offsets, i, a.strip, s, n);
+      uint32_t h = hash_key(s, n, kBloomSeed);
+      const uint32_t delta = (h >> 17) | (h << 15);
+      for (uint32_t j = 0; j < a.k; j++) {
+        const uint64_t rel = (uint64_t)mod_bits(h, m) - bit0;  // wraps below the window
+        if (rel < nbits) atomicOr(&bm[rel >> 5], 1u << (rel & 31u));
+        h += delta;
+      }
+    }
+    wave_phase();
+    store_window(dst + win, bm, wbytes, lane);
+    wave_phase();
+  }
+  if (lane == 0) *reinterpret_cast<gu8>(dst + bytes) = (uint8_t)a.k;  // :50
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// A wave takes kBloomGroup consecutive filters at a time.  When their keys
+// are contiguous and their bit arrays fit one LDS image (db_bench: 16 x 84 B),
+// the keys of all of them are spread over the 64 lanes round by round (33-key
+// filters would leave half the lanes idle at one filter per wave), each lane
+// finds its key's filter among the group, and every filter leaves LDS once.
+// Otherwise the group's filters go one by one through build_one.
 __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildArgs a) {
   __shared__ uint32_t lds[kBloomWaves][kBloomWindowWords + 1];
+  __shared__ uint32_t slot_word[kBloomWaves][kBloomGroup], slot_d[kBloomWaves][kBloomGroup];
+  __shared__ uint64_t slot_m[kBloomWaves][kBloomGroup];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* bm = lds[wv];
   const uint64_t nwaves = (uint64_t)gridDim.x * kBloomWaves;
-  for (uint64_t f = (uint64_t)blockIdx.x * kBloomWaves + wv; f < a.n_filters; f += nwaves) {
-    // util/bloom.cc:39-46: bits = max(64, n * bits_per_key), rounded up to bytes
-    const uint64_t k0 = a.filter_first[f], k1 = a.filter_first[f + 1];
-    const uint64_t nk = k1 > k0 ? k1 - k0 : 0;
-    uint64_t bits = nk * a.bits_per_key;
-    if (bits < 64) bits = 64;
-    const uint64_t bytes = (bits + 7) / 8;
-    const BitMod m = bit_mod(bytes * 8);
-    const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + a.filter_out[f];
-    for (uint64_t win = 0; win < bytes; win += kBloomWindowBytes) {
-      const uint32_t wbytes =
-          (uint32_t)(bytes - win < kBloomWindowBytes ? bytes - win : kBloomWindowBytes);
-      const uint64_t bit0 = win * 8, nbits = (uint64_t)wbytes * 8;
-      for (uint32_t i = lane; i <= wbytes / 4; i += 64) bm[i] = 0;  // + 1 pad word
-      wave_phase();
-      // util/bloom.cc:52-62: double hashing, delta = h rotated right 17
-      for (uint64_t i = k0 + lane; i < k1; i += 64) {
-        uint64_t s, n;
-        key_extent(a.keys, a.key_offsets, i, a.strip, s, n);
-        uint32_t h = hash_key(s, n, kBloomSeed);
-        const uint32_t delta = (h >> 17) | (h << 15);
-        for (uint32_t j = 0; j < a.k; j++) {
-          const uint64_t rel = (uint64_t)mod_bits(h, m) - bit0;  // wraps below the window
-          if (rel < nbits) atomicOr(&bm[rel >> 5], 1u << (rel & 31u));
-          h += delta;
-        }
-      }
-      wave_phase();
-      store_window(dst + win, bm, wbytes, lane);
-      wave_phase();
+  const uint64_t n_groups = (a.n_filters + kBloomGroup - 1) / kBloomGroup;
+  for (uint64_t grp = (uint64_t)blockIdx.x * kBloomWaves + wv; grp < n_groups; grp += nwaves) {
+    const uint64_t f0 = grp * kBloomGroup;
+    const uint32_t g = (uint32_t)(a.n_filters - f0 < kBloomGroup ? a.n_filters - f0 : kBloomGroup);
+    // lane j < g: filter f0 + j
+    uint64_t k0 = 0, k1 = 0, fo = 0, bytes = 0;
+    if (lane < g) {
+      k0 = a.filter_first[f0 + lane];
+      k1 = a.filter_first[f0 + lane + 1];
+      fo = a.filter_out[f0 + lane];
+      uint64_t bits = (k1 > k0 ? k1 - k0 : 0) * a.bits_per_key;
+      if (bits < 64) bits = 64;
+      bytes = (bits + 7) / 8;
     }
-    if (lane == 0) *reinterpret_cast<gu8>(dst + bytes) = (uint8_t)a.k;  // :50
+    // LDS words of each filter (+ 1 pad word for the funnel-shifted store)
+    const uint64_t words = lane < g ? (bytes + 3) / 4 + 1 : 0;
+    uint64_t incl = words;
+#pragma unroll
+    for (uint32_t d = 1; d < kBloomGroup; d <<= 1) {
+      const uint64_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    const uint64_t total = readlane64(incl, kBloomGroup - 1);
+    const uint64_t kb0 = readlane64(k0, 0), kb1 = readlane64(k1, g - 1);
+    const uint64_t next0 = __shfl_down(k0, 1);
+    const bool contiguous = lane >= g || (k1 >= k0 && (lane == g - 1 || next0 == k1));
+    const bool packed = __ballot(!contiguous) == 0 && total <= kBloomWindowWords &&
+                        kb1 >= kb0 && kb1 - kb0 < (1ull << 31);
+    if (!packed) {
+      for (uint32_t j = 0; j < g; j++)
+        build_one(a, readlane64(k0, j), readlane64(k1, j), readlane64(fo, j), bm, lane);
+      continue;
+    }
+    const uint32_t base = (uint32_t)(incl - words);
+    if (lane < g) {
+      const uint32_t d = (uint32_t)(bytes * 8);
+      slot_word[wv][lane] = base;
+      slot_d[wv][lane] = d;
+      slot_m[wv][lane] = fastmod_magic(d);
+    }
+    for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
+    // first key (relative to the group's) of filters 1..g-1, wave-uniform
+    uint32_t st[kBloomGroup];
+#pragma unroll
+    for (uint32_t j = 1; j < kBloomGroup; j++)
+      st[j] = j < g ? (uint32_t)(readlane64(k0, j) - kb0) : 0xffffffffu;
+    wave_phase();
+    const uint32_t nkeys = (uint32_t)(kb1 - kb0);
+    for (uint32_t r = lane; r < nkeys; r += 64) {
+      uint32_t j = 0;
+#pragma unroll
+      for (uint32_t t = 1; t < kBloomGroup; t++) j += r >= st[t] ? 1u : 0u;
+      const uint32_t wbase = slot_word[wv][j], d = slot_d[wv][j];
+      const uint64_t M = slot_m[wv][j];
+      uint64_t s, n;
+      key_extent(a.keys, a.key_offsets, kb0 + r, a.strip, s, n);
+      uint32_t h = hash_key(s, n, kBloomSeed);
+      const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
+      for (uint32_t q = 0; q < a.k; q++) {
+        const uint32_t bitpos = fastmod(h, M, d);
+        atomicOr(&bm[wbase + (bitpos >> 5)], 1u << (bitpos & 31u));
+        h += delta;
+      }
+    }
+    wave_phase();
+    for (uint32_t j = 0; j < g; j++) {
+      const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + readlane64(fo, j);
+      const uint32_t nb = (uint32_t)readlane64(bytes, j);
+      store_window(dst, bm + __builtin_amdgcn_readlane(base, j), nb, lane);
+      if (lane == 0) *reinterpret_cast<gu8>(dst + nb) = (uint8_t)a.k;  // :50
+    }
+    wave_phase();
   }
 }
 
@@ -183,12 +322,25 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
   const uint64_t k = stored > k_use ? k_use : stored;
   if (k > 30) return true;
   const BitMod m = bit_mod((len - 1) * 8);
-  uint32_t h = hash_key(ks, kn, kBloomSeed);
+  uint32_t h = hash_key_batched(ks, kn, kBloomSeed);
   const uint32_t delta = (h >> 17) | (h << 15);
-  for (uint32_t j = 0; j < (uint32_t)k; j++) {
-    const uint32_t bitpos = mod_bits(h, m);
-    if ((*reinterpret_cast<gcu8>(f + (bitpos >> 3)) & (1u << (bitpos & 7u))) == 0) return false;
-    h += delta;
+  // The reference stops at the first clear bit (:85); the answer is the same
+  // if a chunk of up to 16 probe bytes (all inside this filter) is requested
+  // at once and tested together: one round trip instead of up to k.
+  for (uint32_t j0 = 0; j0 < (uint32_t)k; j0 += 16) {
+    uint32_t v[16], bit[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t bitpos = mod_bits(h, m);
+      const bool live = j0 + j < (uint32_t)k;
+      bit[j] = live ? 1u << (bitpos & 7u) : 0u;
+      v[j] = live ? *reinterpret_cast<gcu8>(f + (bitpos >> 3)) : 0u;
+      h += delta;
+    }
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < 16; j++) all &= (v[j] & bit[j]) == bit[j];
+    if (!all) return false;
   }
   return true;
 }

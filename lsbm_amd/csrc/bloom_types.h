@@ -9,6 +9,7 @@ constexpr int kBloomThreads = 256;                 // 4 waves per workgroup
 constexpr int kBloomWaves = kBloomThreads / 64;
 constexpr uint32_t kBloomWindowBytes = 4096;       // filter bytes a wave holds in LDS at once
 constexpr uint32_t kBloomWindowWords = kBloomWindowBytes / 4;
+constexpr uint32_t kBloomGroup = 16;                // filters a wave takes at a time
 
 struct BloomBuildArgs {
   const uint8_t* keys;

@@ -109,4 +109,39 @@ int ref_filter_block_may_match(int bits_per_key, int strip, const char* contents
   return r ? 1 : 0;
 }
 
+// Batch drivers for the CPU baseline (tools/bench_bloom.py): the reference's
+// CreateFilter over n_filters filters of keys [first[f], first[f+1]) (one
+// policy object, as a TableBuilder holds), and KeyMayMatch of key i against
+// filter fidx[i] (filters at fo[f], fo[f+1]); returns the number of matches.
+size_t ref_create_filters(int bits_per_key, const char* keys, const uint64_t* offs,
+                          const uint64_t* first, size_t n_filters, char* out, uint64_t* fo) {
+  const leveldb::FilterPolicy* p = leveldb::NewBloomFilterPolicy(bits_per_key);
+  std::string dst;
+  std::vector<leveldb::Slice> k;
+  fo[0] = 0;
+  for (size_t f = 0; f < n_filters; f++) {
+    k.clear();
+    for (uint64_t i = first[f]; i < first[f + 1]; i++)
+      k.push_back(leveldb::Slice(keys + offs[i], offs[i + 1] - offs[i]));
+    p->CreateFilter(k.empty() ? nullptr : &k[0], (int)k.size(), &dst);
+    fo[f + 1] = dst.size();
+  }
+  delete p;
+  memcpy(out, dst.data(), dst.size());
+  return dst.size();
+}
+
+size_t ref_may_match_batch(int bits_per_key, const char* keys, const uint64_t* offs, size_t n,
+                           const char* filters, const uint64_t* fo, const uint64_t* fidx) {
+  const leveldb::FilterPolicy* p = leveldb::NewBloomFilterPolicy(bits_per_key);
+  size_t hits = 0;
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t f = fidx[i];
+    hits += p->KeyMayMatch(leveldb::Slice(keys + offs[i], offs[i + 1] - offs[i]),
+                           leveldb::Slice(filters + fo[f], fo[f + 1] - fo[f]));
+  }
+  delete p;
+  return hits;
+}
+
 }  // extern "C"

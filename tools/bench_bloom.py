@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Bloom-filter rates on one GPU, db_bench shaped:
+internal keys "user%019d" + 8-byte sequence/type (31 B, lsbm/db_bench.cc:1415),
+33 keys per filter (one ~4 KiB data block per 2 KiB filter slot,
+table/filter_block.cc:14-16), BloomFilterPolicy(20) under InternalFilterPolicy
+(strip 8), config::bloom_bits_use = 15.  Keys are generated on the device and
+resident in HBM before timing.  One JSON line per measurement:
+
+  bloom_build   lsbm_bloom_build_dev over every filter of the batch
+  bloom_probe   lsbm_bloom_may_match_dev, every key against its own filter
+  bloom_block   lsbm_filter_block_may_match_dev, through FilterBlockReader's
+                offset array (one filter block per 1,024 filters)
+
+Algorithmic bytes (what the roofline fraction uses) are stated per line.
+cpu_baseline: the reference's own CreateFilter / KeyMayMatch
+(oracle/_ref/libref_bloom.so, built from /root/reference) on one host core,
+on a bounded sample, else the oracle's C restatement.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+HBM = 8000.0  # GB/s, MI355X spec
+KLEN, PER, BPK = 31, 33, 20
+
+
+def dbbench_keys_dev(torch, n, first=0, seq0=1):
+    nums = torch.arange(first, first + n, dtype=torch.int64, device="cuda")
+    out = torch.empty((n, KLEN), dtype=torch.uint8, device="cuda")
+    out[:, :4] = torch.tensor(list(b"user"), dtype=torch.uint8, device="cuda")
+    for p in range(19):
+        out[:, 4 + p] = (torch.div(nums, 10 ** (18 - p), rounding_mode="floor") % 10 + 48).to(torch.uint8)
+    tag = (torch.arange(seq0, seq0 + n, dtype=torch.int64, device="cuda") << 8) | 1
+    for b in range(8):
+        out[:, 23 + b] = ((tag >> (8 * b)) & 0xFF).to(torch.uint8)
+    return out.reshape(-1)
+
+
+def timed(torch, fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def cpu_baseline(sample_filters, seconds=4.0):
+    """The reference's own CreateFilter / KeyMayMatch loops (C, one thread) on
+    a bounded db_bench-shaped sample, repeated for about `seconds`; the
+    oracle's C restatement when the reference build is absent."""
+    from golden.bloomkeys import dbbench_keys
+    n = sample_filters * PER
+    first = np.minimum(np.arange(sample_filters + 1, dtype=np.uint64) * PER, n).astype(np.uint64)
+    fidx = (np.arange(n) // PER).astype(np.uint64)
+    fo = np.zeros(sample_filters + 1, dtype=np.uint64)
+    out = np.zeros(sample_filters * 100, dtype=np.uint8)
+    vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_bloom.so")
+    if os.path.exists(ref):
+        lib, kind = ctypes.CDLL(ref), "reference"
+        lib.ref_create_filters.restype = sz
+        lib.ref_create_filters.argtypes = [i32, vp, vp, vp, sz, vp, vp]
+        lib.ref_may_match_batch.restype = sz
+        lib.ref_may_match_batch.argtypes = [i32, vp, vp, sz, vp, vp, vp]
+        # InternalFilterPolicy hands the bloom policy user keys: 23 B
+        keys, offs = dbbench_keys(0, n, internal=False)
+
+        def build():
+            lib.ref_create_filters(BPK, keys.ctypes.data, offs.ctypes.data, first.ctypes.data,
+                                   sample_filters, out.ctypes.data, fo.ctypes.data)
+
+        def probe():
+            return lib.ref_may_match_batch(BPK, keys.ctypes.data, offs.ctypes.data, n,
+                                           out.ctypes.data, fo.ctypes.data, fidx.ctypes.data)
+    else:
+        from conftest import BloomOracle
+        o = BloomOracle(os.path.join(REPO, "oracle", "liboracle_bloom.so"))
+        kind = "port"
+        keys, offs = dbbench_keys(0, n)
+        fsize = o.filter_bytes(PER, BPK)
+        fo[:] = np.arange(sample_filters + 1, dtype=np.uint64) * fsize
+
+        def build():
+            for f in range(sample_filters):
+                o.lib.bo_create_filter(keys.ctypes.data, offs[f * PER:].ctypes.data, PER, 8, BPK,
+                                       out.ctypes.data + f * fsize)
+
+        def probe():
+            return sum(o.lib.bo_key_may_match(keys.ctypes.data + int(offs[i]), KLEN, 8,
+                                              out.ctypes.data + int(fidx[i]) * fsize, fsize, BPK, 15)
+                       for i in range(n))
+
+    def rate(fn):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            r = fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                return reps * n / el, r
+    build_rate, _ = rate(build)
+    probe_rate, hits = rate(probe)
+    cpu = ""
+    try:
+        cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except (OSError, IndexError):
+        pass
+    return {"kind": kind, "cores": 1, "build_keys_per_s": round(build_rate, 1),
+            "probe_keys_per_s": round(probe_rate, 1), "members_found": int(hits) == n,
+            "sample": f"{sample_filters} filters x {PER} db_bench keys, CreateFilter and "
+                      f"KeyMayMatch loops in C, one thread, ~{seconds:.0f} s; {cpu}"}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("which", nargs="*", default=["build", "probe", "block"])
+    p.add_argument("--keys", type=int, default=1 << 25)
+    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--cpu-filters", type=int, default=20000)
+    args = p.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from conftest import BloomOracle
+    from golden.bloomkeys import dbbench_keys, take
+    from lsbm_amd import bloom, engine
+    engine.init(0)
+    o = BloomOracle(os.path.join(REPO, "oracle", "liboracle_bloom.so"))
+    n = args.keys
+    nf = (n + PER - 1) // PER
+    keys = dbbench_keys_dev(torch, n)
+    koffs = torch.arange(0, (n + 1) * KLEN, KLEN, dtype=torch.int64, device="cuda")
+    first = torch.clamp(torch.arange(0, nf + 1, dtype=torch.int64, device="cuda") * PER, max=n)
+    counts = (first[1:] - first[:-1]).cpu().numpy()
+    fbytes = np.array([bloom.filter_bytes(c, BPK) for c in np.unique(counts)])
+    size_of = dict(zip(np.unique(counts).tolist(), fbytes.tolist()))
+    sizes = np.array([size_of[c] for c in counts.tolist()], dtype=np.int64)
+    outo_h = np.zeros(nf, dtype=np.int64)
+    outo_h[1:] = np.cumsum(sizes)[:-1]
+    outo = torch.from_numpy(outo_h).to("cuda")
+    total_out = int(sizes.sum())
+    out = torch.empty(total_out, dtype=torch.uint8, device="cuda")
+    lines = []
+
+    def build():
+        bloom.build_filters(keys, koffs, first, outo, out, BPK, strip=8)
+
+    t = timed(torch, build, args.reps)
+    host_out = out.cpu().numpy()
+    rng = np.random.default_rng(9)
+    bad = 0
+    hk = None
+    for f in rng.choice(nf, 32, replace=False):
+        k0, k1 = int(f) * PER, min(n, int(f) * PER + PER)
+        want = o.create_filter(dbbench_keys(k0, k1 - k0, seq0=1 + k0), BPK, 8)
+        bad += int(host_out[outo_h[f]:outo_h[f] + sizes[f]].tobytes() != want)
+    alg = n * KLEN + (n + 1) * 8 + nf * 16 + total_out
+    gbps = alg / t / 1e9
+    lines.append({"bench": "bloom_build", "keys": n, "filters": nf, "keys_per_filter": PER,
+                  "bits_per_key": BPK, "ms": round(t * 1e3, 3), "Gkeys_per_s": round(n / t / 1e9, 2),
+                  "algorithmic_bytes": alg, "GBps": round(gbps, 1),
+                  "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM,
+                               "unit": "GB/s", "frac": round(gbps / HBM, 4)},
+                  "bytes_note": "31 B key + 8 B key offset per key, 16 B per filter, filter bytes written",
+                  "sample_mismatches": bad})
+    fidx = torch.div(torch.arange(n, device="cuda"), PER, rounding_mode="floor")
+    sizes_d = torch.from_numpy(sizes).to("cuda")
+    handles = torch.stack([outo[fidx], sizes_d[fidx]], 1).reshape(-1).contiguous()
+    if "probe" in args.which:
+        may = torch.empty(n, dtype=torch.uint8, device="cuda")
+        n_may = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+        def probe():
+            bloom.may_match(out, handles, keys, koffs, BPK, 15, strip=8, may=may, n_may=n_may)
+
+        t = timed(torch, probe, args.reps)
+        found = int(n_may.item()) // (args.reps + 2)
+        alg = n * (KLEN + 8 + 16 + 1 + bloom.k_probe(BPK, 15))
+        gbps = alg / t / 1e9
+        lines.append({"bench": "bloom_probe", "queries": n, "ms": round(t * 1e3, 3),
+                      "Gqueries_per_s": round(n / t / 1e9, 2), "algorithmic_bytes": alg,
+                      "GBps": round(gbps, 1),
+                      "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM,
+                                   "unit": "GB/s", "frac": round(gbps / HBM, 4)},
+                      "bytes_note": "31 B key + 8 B offset + 16 B handle + 1 B result + k_use probe bytes",
+                      "members_found": found, "no_false_negatives": found == n})
+    if "block" in args.which:
+        # filter blocks of 1,024 filters each: data blocks at 4,096-B strides
+        per_blk = 1024
+        nb = (nf + per_blk - 1) // per_blk
+        blocks, bh = [], []
+        pos = 0
+        for b in range(nb):
+            f0, f1 = b * per_blk, min(nf, b * per_blk + per_blk)
+            data = host_out[outo_h[f0]:outo_h[f1 - 1] + sizes[f1 - 1]]
+            offsets = (outo_h[f0:f1] - outo_h[f0]).astype("<u4")
+            # one 4 KiB data block per filter: filter index = 2 per data block
+            arr = np.zeros(2 * (f1 - f0), dtype="<u4")
+            arr[0::2] = offsets
+            arr[1::2] = np.append(offsets[1:], data.size).astype("<u4")  # odd slots: empty filters
+            tail = np.frombuffer(np.uint32(data.size).tobytes() + bytes([11]), np.uint8)
+            blk = np.concatenate([data, arr.view(np.uint8), tail])
+            blocks.append(blk)
+            bh.append((pos, blk.size))
+            pos += blk.size
+        blob = torch.from_numpy(np.concatenate(blocks)).to("cuda")
+        qb = (fidx // per_blk).cpu().numpy()
+        bhn = np.array(bh, dtype=np.int64)
+        bhandles = torch.from_numpy(bhn[qb].reshape(-1).copy()).to("cuda")
+        doffs = ((fidx % per_blk) * 4096).to(torch.int64)
+        may = torch.empty(n, dtype=torch.uint8, device="cuda")
+        n_may = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+        def block():
+            bloom.filter_block_may_match(blob, bhandles, doffs, keys, koffs, BPK, 15, strip=8,
+                                         may=may, n_may=n_may)
+
+        t = timed(torch, block, args.reps)
+        found = int(n_may.item()) // (args.reps + 2)
+        alg = n * (KLEN + 8 + 16 + 8 + 1 + 8 + 1 + bloom.k_probe(BPK, 15))
+        gbps = alg / t / 1e9
+        lines.append({"bench": "bloom_block", "queries": n, "filter_blocks": nb,
+                      "ms": round(t * 1e3, 3), "Gqueries_per_s": round(n / t / 1e9, 2),
+                      "algorithmic_bytes": alg, "GBps": round(gbps, 1),
+                      "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM,
+                                   "unit": "GB/s", "frac": round(gbps / HBM, 4)},
+                      "bytes_note": "key + offset + block handle + data offset + trailer byte "
+                                    "+ 2 offset words + k byte + k_use probe bytes",
+                      "members_found": found, "no_false_negatives": found == n})
+    cpu = cpu_baseline(args.cpu_filters) if args.cpu_filters else None
+    for ln in lines:
+        if cpu:
+            ln["cpu_baseline"] = cpu
+        print(json.dumps(ln), flush=True)
+
+
+if __name__ == "__main__":
+    main()
