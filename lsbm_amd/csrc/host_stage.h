@@ -4,7 +4,7 @@
 // Every copy goes through a page-locked bounce buffer with hipMemcpyAsync on
 // the caller's stream.  A synchronous hipMemcpy from pageable memory into a
 // buffer that reuses the address of a freed one was measured to leave the
-// next kernel reading the OLD bytes on MI355X (ROCm 7.2; DESIGN.md section 3,
+// next kernel reading the OLD bytes on MI355X (ROCm 7.2; DESIGN.md section 5,
 // "Staging"); the pinned async path is the one the engine's host-staged
 // batches use and never showed it.
 #pragma once
