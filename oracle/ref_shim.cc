@@ -46,4 +46,13 @@ int ref_batch_fixed_mt(const char* base, uint64_t stride, uint64_t len, uint64_t
   return started == threads ? 0 : -1;
 }
 
+// crc32c::Extend(init[i] or 0, base + ext[2i], ext[2i+1]) for n extents, one
+// thread: the reference's per-record loop (WriteRawBlock / EmitPhysicalRecord)
+// as the config-1 CPU baseline (tools/bench_configs.py).
+void ref_batch_extents(const char* base, const uint64_t* ext, const uint32_t* init,
+                       uint32_t* out, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++)
+    out[i] = leveldb::crc32c::Extend(init ? init[i] : 0, base + ext[2 * i], ext[2 * i + 1]);
+}
+
 }  // extern "C"

@@ -6,6 +6,11 @@ host-staged (PCIe-inclusive) rate.  One JSON line per measurement.
   config4   10M blocks, n = min(65536, 512*r + u), r ~ Zipf(0.99) over 1..128,
             u ~ U[0, 511], densely packed at arbitrary alignment (ragged path)
   host      host-staged batches: pinned host buffer -> GPU -> 4 B/block back
+  config1   db_bench's CRC mix (BASELINE.json configs[0]): 45,036
+            SSTable data blocks of 4117-4122 B + 56 index/filter/meta blocks of
+            31-202 KB sealed by lsbm_sst_seal_dev, and 97,597 WAL records of
+            0-2540 B (mean 1270) sealed in a log image by lsbm_log_seal_dev;
+            beside it the reference's own Extend loop on one host core
 
 Lengths are drawn from splitmix64 streams (seed 0x5EED0002), not the survey's
 mt19937_64, so that numpy regenerates them bit for bit; bytes are the on-device
@@ -144,9 +149,75 @@ def host_staged(args):
                               "4 B/block D2H"}), flush=True)
 
 
+def config1(args):
+    import ctypes
+    import torch
+    from golden.splitmix import printable_bytes
+    from lsbm_amd import log, table
+    rng = np.random.default_rng(0xC1)
+    # 45,036 data blocks (4117 x 12,621, 4118 x 21,072, 4119 x 10,203,
+    # 4120 x 1,033, the rest 4121-4122) + 56 index/filter/meta blocks of 31-202 KB
+    sizes = np.array([4117] * 12621 + [4118] * 21072 + [4119] * 10203 + [4120] * 1033 +
+                     [4121] * 60 + [4122] * 47 + list(rng.integers(31 << 10, 202 << 10, 56)),
+                     dtype=np.int64)
+    rng.shuffle(sizes)
+    handles, total = table.layout_blocks(sizes)
+    img = printable_bytes(0xC1, int(total))
+    d = torch.from_numpy(img).to("cuda")
+    dh = torch.from_numpy(np.ascontiguousarray(handles, dtype=np.int64)).to("cuda")
+    types = torch.zeros(sizes.size, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    t_sst = time_launches(lambda: table.seal_blocks(d, dh, types, stream=s), s, reps=10)
+    sealed = d.cpu().numpy()
+    lens = rng.integers(0, 2541, size=97597)
+    pay = printable_bytes(0xC2, int(lens.sum()))
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    wimg, heads = log.layout_records(pay[offs[i]:offs[i + 1]] for i in range(lens.size))
+    dw = torch.from_numpy(wimg).to("cuda")
+    dwh = torch.from_numpy(heads).to("cuda")
+    t_wal = time_launches(lambda: log.seal_records(dw, dwh, stream=s), s, reps=10)
+    wsealed = dw.cpu().numpy()
+    sst_bytes = int(sizes.sum()) + sizes.size  # block || type
+    # reference Extend loop, one core: block || type (WriteRawBlock) and
+    # type_crc_[t] extended over the payload (EmitPhysicalRecord)
+    ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libref_crc32c.so"))
+    ref.ref_batch_extents.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64]
+    ext = np.stack([handles[0::2], handles[1::2] + 1], 1).astype(np.uint64).reshape(-1)
+    out = np.empty(sizes.size, dtype=np.uint32)
+    t0 = time.perf_counter()
+    ref.ref_batch_extents(sealed.ctypes.data, ext.ctypes.data, None, out.ctypes.data, sizes.size)
+    c_sst = time.perf_counter() - t0
+    plen = (wsealed[heads + 4].astype(np.uint64) | (wsealed[heads + 5].astype(np.uint64) << 8))
+    wext = np.stack([heads.astype(np.uint64) + 6, plen + 1], 1).reshape(-1)
+    wout = np.empty(heads.size, dtype=np.uint32)
+    t0 = time.perf_counter()
+    ref.ref_batch_extents(wsealed.ctypes.data, wext.ctypes.data, None, wout.ctypes.data, heads.size)
+    c_wal = time.perf_counter() - t0
+    o = oracle()
+    # the GPU's trailers / headers are what the reference computes
+    bad = sum(int(o.mask(int(out[i])) != int.from_bytes(sealed[handles[2 * i] + sizes[i] + 1:
+                                                               handles[2 * i] + sizes[i] + 5].tobytes(),
+                                                        "little"))
+              for i in range(0, sizes.size, 97))
+    bad += sum(int(o.mask(int(wout[i])) != int.from_bytes(wsealed[heads[i]:heads[i] + 4].tobytes(), "little"))
+               for i in range(0, heads.size, 97))
+    crc_bytes = sst_bytes + int(plen.sum()) + heads.size
+    print(json.dumps({"config": "config1", "sst_blocks": int(sizes.size), "sst_crc_bytes": sst_bytes,
+                      "wal_records": int(lens.size), "wal_physical": int(heads.size),
+                      "wal_crc_bytes": int(plen.sum()) + int(heads.size),
+                      "gpu_ms": {"sst_seal": round(t_sst * 1e3, 3), "log_seal": round(t_wal * 1e3, 3)},
+                      "gpu_GBps": round(crc_bytes / (t_sst + t_wal) / 1e9, 1),
+                      "cpu_reference_1core": {"s": round(c_sst + c_wal, 4),
+                                              "GBps": round(crc_bytes / (c_sst + c_wal) / 1e9, 3)},
+                      "speedup_vs_1core": round((c_sst + c_wal) / (t_sst + t_wal), 1),
+                      "sample_mismatches": bad,
+                      "note": "device-resident images; the reference run writes these through "
+                              "fwrite on one thread (SURVEY.md 3.5)"}), flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("which", nargs="*", default=["config3", "config4", "host"])
+    p.add_argument("which", nargs="*", default=["config1", "config3", "config4", "host"])
     p.add_argument("--c3-blocks", type=int, default=1 << 20)
     p.add_argument("--c4-blocks", type=int, default=10_000_000)
     p.add_argument("--host-blocks", type=int, default=1 << 18)
@@ -156,7 +227,7 @@ def main():
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"config3": config3, "config4": config4, "host": host_staged}[w](args)
+        {"config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
 
 
 if __name__ == "__main__":

@@ -9,6 +9,6 @@ echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-2500
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/bench_configs.py ${CONFIGS:-config3 config4 host} > gpurun_out/configs.log 2>&1
+timeout -k 10 300 python -u tools/bench_configs.py ${CONFIGS:-config1 config3 config4 host} > gpurun_out/configs.log 2>&1
 rc=$?; echo "configs rc=$rc"; grep '^{' gpurun_out/configs.log
 exit $rc
