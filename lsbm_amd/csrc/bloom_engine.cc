@@ -49,7 +49,9 @@ int probe(const uint8_t* base, const uint64_t* handles, const uint64_t* data_off
   a.k_use = lsbm_bloom_k_probe(bits_per_key, bloom_bits_use);
   a.strip = strip;
   a.mode = mode;
-  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, 8), static_cast<hipStream_t>(stream));
+  // grid-stride: no more workgroups than are resident at once (98 VGPRs ->
+  // 4 waves per SIMD = 4 workgroups of 256 per CU; hipcc -Rpass-analysis)
+  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, 4), static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_probe_kernel");
 }
 
@@ -81,9 +83,11 @@ __attribute__((visibility("default"))) int lsbm_bloom_build_dev(
   a.bits_per_key = (uint64_t)bits_per_key;
   a.strip = strip;
   a.k = lsbm_bloom_k(bits_per_key);
-  // one wave per group of kBloomGroup filters; up to 8 workgroups of 4 waves per CU
+  // one wave per group of kBloomGroup filters; grid-stride with no more
+  // workgroups than are resident at once (106 SGPRs -> 6 workgroups of 256 per
+  // CU, MI355X_MICROARCH.md "Residency"; hipcc -Rpass-analysis)
   const uint64_t groups = (n_filters + kBloomGroup - 1) / kBloomGroup;
-  const hipError_t e = launch_bloom_build(a, grid_for(cus, groups, kBloomWaves, 8),
+  const hipError_t e = launch_bloom_build(a, grid_for(cus, groups, kBloomWaves, 6),
                                           static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_build_kernel");
 }

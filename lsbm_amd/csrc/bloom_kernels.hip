@@ -152,6 +152,24 @@ __device__ __forceinline__ uint32_t fastmod(uint32_t n, uint64_t M, uint32_t d) 
   return (uint32_t)((hi + (lo >> 32)) >> 32);  // high 64 bits of low * d
 }
 
+// The probe positions of util/bloom.cc:57-61 / :83-87 are h_j mod d with
+// h_{j+1} = h_j + delta (mod 2^32).  So after the first one,
+//   h_{j+1} mod d = (h_j mod d + delta mod d - wrap_j * (2^32 mod d)) mod d,
+// wrap_j = carry out of h_j + delta: two remainders per key instead of k,
+// then one add, one compare and a rare correction per probe.  Needs d < 2^31.
+struct ProbeSeq {
+  uint32_t pos, dm, c32, d, h, delta;
+  __device__ __forceinline__ void next() {
+    const uint32_t hn = h + delta;
+    const bool wrap = hn < h;
+    h = hn;
+    uint32_t p = pos + dm;
+    if (p >= d) p -= d;
+    if (wrap) p = p >= c32 ? p - c32 : p + (d - c32);
+    pos = p;
+  }
+};
+
 // Orders one wave's LDS phases (its own ds ops complete in order; this keeps
 // the compiler from moving accesses across the phase boundary).
 __device__ __forceinline__ void wave_phase() {
@@ -229,6 +247,7 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
   __shared__ uint32_t lds[kBloomWaves][kBloomWindowWords + 1];
   __shared__ uint32_t slot_word[kBloomWaves][kBloomGroup], slot_d[kBloomWaves][kBloomGroup];
   __shared__ uint64_t slot_m[kBloomWaves][kBloomGroup];
+  __shared__ uint32_t slot_c32[kBloomWaves][kBloomGroup];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* bm = lds[wv];
@@ -271,7 +290,10 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
       const uint32_t d = (uint32_t)(bytes * 8);
       slot_word[wv][lane] = base;
       slot_d[wv][lane] = d;
-      slot_m[wv][lane] = fastmod_magic(d);
+      const uint64_t M = fastmod_magic(d);
+      slot_m[wv][lane] = M;
+      const uint32_t c = fastmod(0xffffffffu, M, d) + 1;  // 2^32 mod d
+      slot_c32[wv][lane] = c == d ? 0 : c;
     }
     for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
     // first key (relative to the group's) of filters 1..g-1, wave-uniform
@@ -281,20 +303,33 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
       st[j] = j < g ? (uint32_t)(readlane64(k0, j) - kb0) : 0xffffffffu;
     wave_phase();
     const uint32_t nkeys = (uint32_t)(kb1 - kb0);
+    // The build is latency-bound (PMC: waves wait 74% of their cycles): the
+    // next round's key offsets are loaded while this round hashes, and a key's
+    // words are all requested at once (hash_key_batched).
+    const uint64_t* ko = a.key_offsets + kb0;
+    uint64_t o0 = 0, o1 = 0;
+    if (lane < nkeys) {
+      o0 = ko[lane];
+      o1 = ko[lane + 1];
+    }
     for (uint32_t r = lane; r < nkeys; r += 64) {
       uint32_t j = 0;
 #pragma unroll
       for (uint32_t t = 1; t < kBloomGroup; t++) j += r >= st[t] ? 1u : 0u;
       const uint32_t wbase = slot_word[wv][j], d = slot_d[wv][j];
       const uint64_t M = slot_m[wv][j];
-      uint64_t s, n;
-      key_extent(a.keys, a.key_offsets, kb0 + r, a.strip, s, n);
-      uint32_t h = hash_key(s, n, kBloomSeed);
+      const uint64_t s = reinterpret_cast<uint64_t>(a.keys) + o0;
+      const uint64_t n = o1 >= o0 + a.strip ? o1 - o0 - a.strip : 0;  // key_extent
+      if (r + 64 < nkeys) {
+        o0 = ko[r + 64];
+        o1 = ko[r + 65];
+      }
+      uint32_t h = hash_key_batched(s, n, kBloomSeed);
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
+      ProbeSeq ps{fastmod(h, M, d), fastmod(delta, M, d), slot_c32[wv][j], d, h, delta};
       for (uint32_t q = 0; q < a.k; q++) {
-        const uint32_t bitpos = fastmod(h, M, d);
-        atomicOr(&bm[wbase + (bitpos >> 5)], 1u << (bitpos & 31u));
-        h += delta;
+        atomicOr(&bm[wbase + (ps.pos >> 5)], 1u << (ps.pos & 31u));
+        ps.next();
       }
     }
     wave_phase();
@@ -321,9 +356,18 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
   const uint64_t stored = (uint64_t)(int64_t)(int8_t)*reinterpret_cast<gcu8>(f + len - 1);
   const uint64_t k = stored > k_use ? k_use : stored;
   if (k > 30) return true;
-  const BitMod m = bit_mod((len - 1) * 8);
+  const uint64_t bits = (len - 1) * 8;
+  const BitMod m = bit_mod(bits);
   uint32_t h = hash_key_batched(ks, kn, kBloomSeed);
   const uint32_t delta = (h >> 17) | (h << 15);
+  const bool inc = bits < (1ull << 31);  // ProbeSeq's range; else a remainder per probe
+  ProbeSeq ps{0, 0, 0, (uint32_t)bits, h, delta};
+  if (inc) {
+    ps.pos = mod_bits(h, m);
+    ps.dm = mod_bits(delta, m);
+    const uint32_t c = mod_bits(0xffffffffu, m) + 1;  // 2^32 mod bits
+    ps.c32 = c == ps.d ? 0 : c;
+  }
   // The reference stops at the first clear bit (:85); the answer is the same
   // if a chunk of up to 16 probe bytes (all inside this filter) is requested
   // at once and tested together: one round trip instead of up to k.
@@ -331,11 +375,12 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
     uint32_t v[16], bit[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      const uint32_t bitpos = mod_bits(h, m);
+      const uint32_t bitpos = inc ? ps.pos : mod_bits(ps.h, m);
       const bool live = j0 + j < (uint32_t)k;
       bit[j] = live ? 1u << (bitpos & 7u) : 0u;
       v[j] = live ? *reinterpret_cast<gcu8>(f + (bitpos >> 3)) : 0u;
-      h += delta;
+      if (inc) ps.next();
+      else ps.h += delta;
     }
     bool all = true;
 #pragma unroll
