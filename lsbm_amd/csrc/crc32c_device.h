@@ -25,6 +25,8 @@
 //   0x20000        nibble tables of A^4 (16 entries each: conflict-free)
 //   0x20800        nibble tables of A^(116-16li), replicated per lane slot
 //                  (lane & 31) like the byte tables: conflict-free.
+//   kNibRowPow     nibble tables of A^(128 * 2^i), i < 21 (ragged-path unit shifts)
+//   kNibNeg4       nibble tables of A^-4 (init injection)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -83,8 +83,8 @@ void build_consts(DevConsts* c) {
     const uint32_t q = w >> 9, nib = (w >> 5) & 15u, slot = w & 31u;
     c->lds_image[kNibFin / 4 + w] = c->fin_nib[slot & 7u][q * 16 + nib];
   }
-  for (uint32_t i = 0; i < 16; i++)  // A^(4096 * 2^i) = A^(2^(12+i))
-    memcpy(&c->lds_image[kNibU4096 / 4 + i * 128], c->pow_nib[12 + i], 512);
+  for (uint32_t i = 0; i < kRowPowTables; i++)  // A^(128 * 2^i) = A^(2^(7+i))
+    memcpy(&c->lds_image[kNibRowPow / 4 + i * 128], c->pow_nib[7 + i], 512);
   memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
   memset(c->zero16, 0, sizeof(c->zero16));
 }

@@ -283,6 +283,7 @@ __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b,
 struct Frame {
   uint64_t s, e, row0, rows;  // rows >= 1
   uint32_t units;             // ceil(rows / 32)
+  uint32_t q, rem;            // balanced split: units of q rows, the first rem of them q + 1
 };
 
 __device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e) {
@@ -293,6 +294,9 @@ __device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e) {
   const uint64_t row_end = (e + 127) >> 7;
   f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
   f.units = (uint32_t)((f.rows + kUnitRows - 1) / kUnitRows);
+  // rows < 2^32 (blocks under 512 GiB): 32-bit division
+  f.q = (uint32_t)f.rows / f.units;
+  f.rem = (uint32_t)f.rows - f.q * f.units;
   return f;
 }
 
@@ -307,11 +311,12 @@ __device__ __forceinline__ uint32_t nib_lds_at(const uint32_t* lds, uint32_t tab
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
-// A^(4096 k)(v): LDS tables for bits 0..15 of k, global ones beyond.
-__device__ __forceinline__ uint32_t shift_units(const uint32_t* lds, const DevConsts* dc,
-                                                uint32_t v, uint64_t k) {
+// A^(128 k)(v), k rows: LDS tables for bits 0..kRowPowTables-1 of k, global ones beyond.
+__device__ __forceinline__ uint32_t shift_rows(const uint32_t* lds, const DevConsts* dc,
+                                               uint32_t v, uint64_t k) {
   for (uint32_t i = 0; k; i++, k >>= 1)
-    if (k & 1u) v = i < 16 ? nib_lds_at(lds, kNibU4096 + i * 512, v) : nib_glb(dc->pow_nib[12 + i], v);
+    if (k & 1u)
+      v = i < kRowPowTables ? nib_lds_at(lds, kNibRowPow + i * 512, v) : nib_glb(dc->pow_nib[7 + i], v);
   return v;
 }
 
@@ -360,7 +365,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   load_lds_tables(g_lds, dc);  // overlaps the first extents' latency
 
   // the previous round's braids and destination
-  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, pk = 0;
+  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+  uint64_t pk = 0;
   uint64_t pb = 0;
   bool pact = false;
   auto retire = [&]() {  // merge the previous round's braids into acc
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
 #endif
     if (pact) {
-      const uint32_t contrib = shift_units(g_lds, dc, raw, pk);
+      const uint32_t contrib = shift_rows(g_lds, dc, raw, pk);
 #ifdef LSBM_DEBUG_BOUNDS
       if (li == 0 && pb >= args.n) printf("ACC OOB wave %lu b %lu n %lu\n", (unsigned long)wave, (unsigned long)pb, (unsigned long)args.n);
       else
@@ -411,12 +417,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint32_t pre_before = jg ? pre_prev : 0u;
     const uint64_t b = cur_b + jg;
     const bool active = jg < 9 && b < b_hi;
-    Frame f = {0, 0, 0, 1, 1};
+    Frame f = {0, 0, 0, 1, 1, 1, 0};
     f.s = __shfl((unsigned long long)ft.s, (int)jg);
     f.e = __shfl((unsigned long long)ft.e, (int)jg);
     f.row0 = __shfl((unsigned long long)ft.row0, (int)jg);
     f.rows = __shfl((unsigned long long)ft.rows, (int)jg);
     f.units = (uint32_t)__shfl((int)ft.units, (int)jg);
+    f.q = (uint32_t)__shfl((int)ft.q, (int)jg);
+    f.rem = (uint32_t)__shfl((int)ft.rem, (int)jg);
     const uint32_t iv = (uint32_t)__shfl((int)ivj, (int)jg);
     const uint32_t o = my_t - pre_before;
     // the cursor after these 8 units, and the next round's extents
@@ -428,7 +436,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     uint32_t ivn;
     prefetch(nb, rn, ivn);
 
-    uint32_t rows = 0, k = 0;
+    uint32_t rows = 0;
+    uint64_t k = 0;  // rows of the frame after this unit
     uint64_t row_a = dummy;  // absolute address of this lane's slice of the unit's first row
     uint64_t r0 = 0;
     // rows whose loads are inside [s, e): [r_lo, r_hi).  Per lane at most two
@@ -439,11 +448,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     uint32_t r_lo = 0, r_hi = 0, rfs = ~0u, rfe = ~0u;
     int32_t ds = -64, de_s = 64, de_e = 64;
     if (active) {
-      const uint32_t first_rows = (uint32_t)(f.rows - (uint64_t)kUnitRows * (f.units - 1));
-      rows = o == 0 ? first_rows : kUnitRows;
-      r0 = f.row0 + (o == 0 ? 0 : first_rows + (uint64_t)kUnitRows * (o - 1));
+      // balanced units: a 4,118-B SSTable block (33-34 rows) is 17 + 17 rows,
+      // not 2 + 32, so a round of 8 such units runs 17 row steps, not 32
+      const uint64_t start = (uint64_t)o * f.q + (o < f.rem ? o : f.rem);
+      rows = f.q + (o < f.rem ? 1u : 0u);
+      r0 = f.row0 + start;
       row_a = r0 * kRowBytes + 16u * li;
-      k = f.units - 1 - o;
+      k = f.rows - start - rows;
       const bool edge = r0 * kRowBytes < f.s || (r0 + rows) * kRowBytes > f.e;
       r_hi = rows;
       if (edge) {

@@ -17,8 +17,9 @@ constexpr uint32_t kLdsByteTabBytes = 131072;
 constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
 constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
                                          // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
-constexpr uint32_t kNibU4096 = kNibFin + 8 * 16 * 32 * 4;  // A^(4096 * 2^i), i = 0..15
-constexpr uint32_t kNibNeg4 = kNibU4096 + 16 * 512;  // A^-4 (init injection)
+constexpr uint32_t kRowPowTables = 21;
+constexpr uint32_t kNibRowPow = kNibFin + 8 * 16 * 32 * 4;  // A^(128 * 2^i), i = 0..20
+constexpr uint32_t kNibNeg4 = kNibRowPow + kRowPowTables * 512;  // A^-4 (init injection)
 constexpr uint32_t kLdsBytes = kNibNeg4 + 512;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
@@ -54,10 +55,10 @@ enum RaggedMode : uint32_t {
   kModeLogVerify = 5,  // ok[i] = Unmask(header[0..4)) == crc(type || payload)
 };
 
-// Ragged path: a block's 128-B-aligned frame [row0, row_end) is cut into
-// units of at most kUnitRows rows: ordinal 0 is the (possibly short) unit at
-// the frame start, ordinals 1..m-1 are full units.  A unit's raw CRC is
-// shifted to the frame end with A^(4096 * k), k = m - 1 - ordinal.
+// Ragged path: a block's 128-B-aligned frame [row0, row_end) of R rows is cut
+// into m = ceil(R / kUnitRows) units of near-equal size (R / m rows, the first
+// R % m of them one more).  A unit's raw CRC is shifted to the frame end with
+// A^(128 k), k = the frame's rows after the unit.
 constexpr uint32_t kUnitRows = 32;
 
 struct RaggedArgs {
