@@ -286,14 +286,14 @@ struct Frame {
   uint32_t q, rem;            // balanced split: units of q rows, the first rem of them q + 1
 };
 
-__device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e) {
+__device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e, uint32_t max_rows = kUnitRows) {
   Frame f;
   f.s = s;
   f.e = e;
   f.row0 = (s - 4) >> 7;
   const uint64_t row_end = (e + 127) >> 7;
   f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
-  f.units = (uint32_t)((f.rows + kUnitRows - 1) / kUnitRows);
+  f.units = (uint32_t)((f.rows + max_rows - 1) / max_rows);
   // rows < 2^32 (blocks under 512 GiB): 32-bit division
   f.q = (uint32_t)f.rows / f.units;
   f.rem = (uint32_t)f.rows - f.q * f.units;
@@ -326,6 +326,11 @@ __device__ __forceinline__ uint32_t shift_rows(const uint32_t* lds, const DevCon
 //   * the extents of the next round's blocks are loaded one round ahead;
 //   * a round issues its first bank of row loads, THEN merges the previous
 //     round's braids (LDS work overlapping the loads), then streams its rows.
+//
+// kMaxRows is the longest unit: kUnitRows for general batches; kSstUnitRows for
+// SSTable trailers, whose blocks (4,117-4,123 B with the type byte, 33-34 rows)
+// then go through as ONE unit each, 8 blocks per round, no split and no shift.
+template <uint32_t kMaxRows>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
   const DevConsts* __restrict__ dc = args.dc;
   const uint32_t lane = threadIdx.x & 63u;
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     // the extents arrived during the previous round.
     uint64_t sj = 0, ej = 0;
     extent_from_raw(args, cur_b + lane, rj, sj, ej);
-    const Frame ft = frame_of(sj, ej);
+    const Frame ft = frame_of(sj, ej, kMaxRows);
     const bool vj = lane < 9u && cur_b + lane < b_hi;
     const uint32_t units_j = vj ? ft.units : 0u;
     uint32_t pre = units_j;
@@ -566,10 +571,10 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     uint32_t dz = wl.z & ~low_bytes(min(max(de_e - 8, 0), 4));
     uint32_t dw = wl.w & ~low_bytes(min(max(de_e - 12, 0), 4));
     asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(dw));
-    // fully unrolled (rows_max <= kUnitRows): a rolled loop got a vmcnt(0) at
+    // fully unrolled (rows_max <= kMaxRows): a rolled loop got a vmcnt(0) at
     // its header, draining the bank in flight every 8 rows
 #pragma unroll
-    for (uint32_t r = 4; r < kUnitRows; r += 8) {
+    for (uint32_t r = 4; r < kMaxRows; r += 8) {
       if (r >= rows_max) break;
 #pragma unroll
       for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(r + 4 + k2));
@@ -777,7 +782,10 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
 
 // acc must hold n zeroed words.
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32c_units_kernel, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+  if (a.mode == kModeSstSeal || a.mode == kModeSstVerify)
+    hipLaunchKernelGGL(crc32c_units_kernel<kSstUnitRows>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL(crc32c_units_kernel<kUnitRows>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t fin_wgs = (a.n + 255) / 256;

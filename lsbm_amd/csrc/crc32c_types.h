@@ -60,6 +60,7 @@ enum RaggedMode : uint32_t {
 // R % m of them one more).  A unit's raw CRC is shifted to the frame end with
 // A^(128 k), k = the frame's rows after the unit.
 constexpr uint32_t kUnitRows = 32;
+constexpr uint32_t kSstUnitRows = 40;  // SSTable trailer modes: a ~4 KiB block is one unit
 
 struct RaggedArgs {
   const uint8_t* base;      // extents are byte offsets from here

@@ -170,8 +170,22 @@ def sst4118(args):
     bad = sum(int(got[b] != o.value(stream_bytes(0x5EED0005, int(offs[b]), L + 1).tobytes()))
               for b in rng.choice(n, 64, replace=False))
     gbps = n * (L + 1) / t / 1e9
+    # the SSTable entry points on the same image: WriteRawBlock seal, ReadBlock verify
+    from lsbm_amd import table
+    handles = torch.from_numpy(np.stack([offs[:-1], np.full(n, L, dtype=np.int64)], 1)
+                               .reshape(-1).copy()).to("cuda")
+    types = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    t_seal = time_launches(lambda: table.seal_blocks(d, handles, types, stream=s), s, reps=10)
+    t_ver = time_launches(lambda: table.verify_blocks(d, handles, stream=s), s, reps=10)
+    ok, nbad = table.verify_blocks(d, handles, stream=s)
+    g_seal, g_ver = n * (L + 1) / t_seal / 1e9, n * (L + 1) / t_ver / 1e9
     print(json.dumps({"config": "sst4118", "blocks": n, "block_bytes": L + 1, "ms": round(t * 1e3, 3),
                       "GBps": round(gbps, 1), "pct_hbm_peak": round(100 * gbps / HBM, 2),
+                      "sst_seal": {"ms": round(t_seal * 1e3, 3), "GBps": round(g_seal, 1),
+                                   "pct_hbm_peak": round(100 * g_seal / HBM, 2)},
+                      "sst_verify": {"ms": round(t_ver * 1e3, 3), "GBps": round(g_ver, 1),
+                                     "pct_hbm_peak": round(100 * g_ver / HBM, 2),
+                                     "all_ok": bool(ok.all()) and int(nbad.item()) == 0},
                       "sample_mismatches": bad}), flush=True)
 
 
