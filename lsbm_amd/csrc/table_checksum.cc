@@ -85,20 +85,11 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
   if (!s.ok()) return s;
   if (lsbm_sst_seal_dev(d.file, d.handles, d.aux, n, d.stream.get()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
-  // bring back only the trailers: gather them on the device side of the
-  // bounce, one 5-byte piece per block
-  std::vector<uint8_t> trailers(n * kBlockTrailerSize);
-  hipError_t e = hipSuccess;
-  for (size_t i = 0; e == hipSuccess && i < n; i++) {
-    const uint64_t t = handles[i].offset + handles[i].size;
-    e = hipMemcpyAsync(trailers.data() + i * kBlockTrailerSize, d.file + t, kBlockTrailerSize,
-                       hipMemcpyDeviceToHost, d.stream.get());
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(d.stream.get());
+  // Bring the image back whole through the pinned bounce: one streamed copy
+  // instead of one 5-byte hipMemcpyAsync (a runtime call) per block.  The
+  // device image is the host image plus the trailers.
+  const hipError_t e = d.bounce.to_host(file, d.file, file_size, d.stream.get());
   if (e != hipSuccess) return hip_status(e, "seal");
-  for (size_t i = 0; i < n; i++)
-    memcpy(file + handles[i].offset + handles[i].size, trailers.data() + i * kBlockTrailerSize,
-           kBlockTrailerSize);
   return Status::OK();
 }
 
