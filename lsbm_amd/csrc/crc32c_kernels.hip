@@ -41,6 +41,10 @@ extern "C" __attribute__((visibility("default"))) int lsbm_diag_stamps(uint64_t*
 #endif
 constexpr uint32_t kPF = LSBM_PF;  // rows per load bank
 
+#ifndef LSBM_UNIT_ROWS  // longest unit of general ragged batches (ablation builds override)
+#define LSBM_UNIT_ROWS kUnitRows
+#endif
+
 constexpr int kAuxNT = 2;     // buffer-load cache policy: non-temporal (read-once stream)
 
 // Issue the loads of rows [r0, r0 + kPF) of this lane's slice into bank X.
@@ -282,7 +286,7 @@ __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b,
 
 struct Frame {
   uint64_t s, e, row0, rows;  // rows >= 1
-  uint32_t units;             // ceil(rows / 32)
+  uint32_t units;             // ceil(rows / max_rows)
   uint32_t q, rem;            // balanced split: units of q rows, the first rem of them q + 1
 };
 
@@ -785,7 +789,7 @@ hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
   if (a.mode == kModeSstSeal || a.mode == kModeSstVerify)
     hipLaunchKernelGGL(crc32c_units_kernel<kSstUnitRows>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
   else
-    hipLaunchKernelGGL(crc32c_units_kernel<kUnitRows>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+    hipLaunchKernelGGL(crc32c_units_kernel<LSBM_UNIT_ROWS>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t fin_wgs = (a.n + 255) / 256;

@@ -59,7 +59,7 @@ enum RaggedMode : uint32_t {
 // into m = ceil(R / kUnitRows) units of near-equal size (R / m rows, the first
 // R % m of them one more).  A unit's raw CRC is shifted to the frame end with
 // A^(128 k), k = the frame's rows after the unit.
-constexpr uint32_t kUnitRows = 32;
+constexpr uint32_t kUnitRows = 48;  // A/B 24..96 rows: plateau from 48
 constexpr uint32_t kSstUnitRows = 40;  // SSTable trailer modes: a ~4 KiB block is one unit
 
 struct RaggedArgs {
