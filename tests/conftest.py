@@ -88,6 +88,58 @@ class Oracle:
         return out
 
 
+class SnappyOracle:
+    """ctypes view of oracle/liboracle_snappy.so (libsnappy's raw format and
+    compressor restated in C, pinned to the libsnappy inside pyarrow)."""
+
+    def __init__(self, path):
+        lib = ctypes.CDLL(path)
+        u32, u64, vp, i = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
+        lib.so_max_compressed_length.restype = u64
+        lib.so_max_compressed_length.argtypes = [u64]
+        lib.so_get_uncompressed_length.restype = i
+        lib.so_get_uncompressed_length.argtypes = [vp, u64, ctypes.POINTER(u32)]
+        lib.so_uncompress.restype = i
+        lib.so_uncompress.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
+        lib.so_compress.restype = u64
+        lib.so_compress.argtypes = [vp, u32, vp]
+        lib.so_compress_batch.restype = None
+        lib.so_compress_batch.argtypes = [vp, vp, u64, vp, vp, vp]
+        lib.so_uncompress_batch.restype = u64
+        lib.so_uncompress_batch.argtypes = [vp, vp, u64, vp, vp, vp]
+        self.lib = lib
+
+    def max_compressed_length(self, n):
+        return self.lib.so_max_compressed_length(n)
+
+    def uncompressed_length(self, c):
+        """(ok, ulength) of snappy::GetUncompressedLength."""
+        b = np.frombuffer(bytes(c) + b"\0", np.uint8)
+        v = ctypes.c_uint32(0)
+        ok = self.lib.so_get_uncompressed_length(b.ctypes.data, len(c), ctypes.byref(v))
+        return bool(ok), v.value if ok else 0
+
+    def compress(self, d):
+        d = bytes(d)
+        src = np.frombuffer(d + b"\0", np.uint8)
+        out = np.zeros(self.max_compressed_length(len(d)) + 8, np.uint8)
+        n = self.lib.so_compress(src.ctypes.data, len(d), out.ctypes.data)
+        return out[:n].tobytes()
+
+    def uncompress(self, c, cap=None):
+        """(ok, output) of snappy::RawUncompress."""
+        c = bytes(c)
+        ok, ulen = self.uncompressed_length(c)
+        if not ok:
+            return False, b""
+        cap = ulen if cap is None else cap
+        src = np.frombuffer(c + b"\0", np.uint8)
+        out = np.zeros(max(cap, 1), np.uint8)
+        got = ctypes.c_uint64(0)
+        ok = self.lib.so_uncompress(src.ctypes.data, len(c), out.ctypes.data, cap, ctypes.byref(got))
+        return (True, out[:got.value].tobytes()) if ok else (False, b"")
+
+
 class BloomOracle:
     """ctypes view of oracle/liboracle_bloom.so (util/hash.cc, util/bloom.cc,
     table/filter_block.cc restated in C).  Keys are (uint8 buffer, uint64
@@ -175,6 +227,17 @@ def oracle():
 @pytest.fixture(scope="session")
 def bloom_oracle():
     return BloomOracle(_build("oracle", "liboracle_bloom.so"))
+
+
+@pytest.fixture(scope="session")
+def snappy_oracle():
+    return SnappyOracle(_build("oracle", "liboracle_snappy.so"))
+
+
+@pytest.fixture(scope="session")
+def snappy_golden():
+    with open(os.path.join(TESTS, "golden", "snappy_fixture.json")) as f:
+        return json.load(f)
 
 
 @pytest.fixture(scope="session")
