@@ -5,10 +5,11 @@
   lsbm_amd.table    SSTable block trailers: batched WriteRawBlock / ReadBlock verify
   lsbm_amd.log      WAL / MANIFEST record CRCs: batched log::Writer seal / log::Reader check
   lsbm_amd.bloom    SSTable bloom filters: batched CreateFilter / KeyMayMatch / filter blocks
+  lsbm_amd.snappy   SSTable block compression: batched snappy RawCompress / RawUncompress
 
 The compute lives in lsbm_amd/liblsbm_crc32c.so (hand-written gfx950 HIP
-kernels behind the C ABIs in include/lsbm_crc32c.h and include/lsbm_bloom.h).
+kernels behind the C ABIs in include/lsbm_crc32c.h, include/lsbm_bloom.h and include/lsbm_snappy.h).
 """
 from ._lib import LIB_PATH, LsbmError, lib  # noqa: F401
 
-__all__ = ["LIB_PATH", "LsbmError", "lib", "crc32c", "engine", "table", "log", "bloom"]
+__all__ = ["LIB_PATH", "LsbmError", "lib", "crc32c", "engine", "table", "log", "bloom", "snappy"]

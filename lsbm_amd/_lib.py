@@ -56,6 +56,10 @@ SIGNATURES = {
                                         _vp]),
     "lsbm_filter_block_may_match_dev": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u64, _int, _int,
                                                _vp, _vp, _vp]),
+    "lsbm_snappy_max_compressed_length": (_u64, [_u64]),
+    "lsbm_snappy_compress_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp]),
+    "lsbm_snappy_uncompressed_length_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp]),
+    "lsbm_snappy_uncompress_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

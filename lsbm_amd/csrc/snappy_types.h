@@ -1,0 +1,49 @@
+// snappy_types.h -- argument blocks shared by snappy_engine.cc (host) and
+// snappy_kernels.hip (device).  Plain C++, no HIP headers.
+#pragma once
+#include <stdint.h>
+
+namespace lsbm {
+
+// One wave per block, one wave per workgroup.  A block whose working set fits
+// the wave's LDS slice is decoded / encoded in LDS; a larger one runs the same
+// algorithm against global memory (output, and the encoder's hash table in a
+// per-workgroup scratch slice).
+constexpr uint32_t kSnapThreads = 64;
+constexpr uint32_t kSnapDecLds = 16384;  // decoder: compressed bytes + 8 pad + output window
+constexpr uint32_t kSnapEncLds = 24576;  // encoder: hash table (2 B/entry) + fragment bytes
+constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
+constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
+constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
+constexpr uint32_t kSnapDecWgsPerCu = 160 * 1024 / kSnapDecLds;  // LDS-limited residency
+constexpr uint32_t kSnapEncWgsPerCu = 160 * 1024 / kSnapEncLds;
+
+struct SnapLenArgs {
+  const uint8_t* base;
+  const uint64_t* offsets;  // block i = base[offsets[i], offsets[i+1])
+  uint64_t* ulen;           // GetUncompressedLength result (0 on failure)
+  uint8_t* ok;
+  uint64_t n;
+};
+
+struct SnapDecArgs {
+  const uint8_t* base;
+  const uint64_t* offsets;      // compressed block i = base[offsets[i], offsets[i+1])
+  uint8_t* out;
+  const uint64_t* out_offsets;  // output i = out[out_offsets[i], out_offsets[i+1]) (capacity)
+  uint8_t* ok;
+  uint32_t* n_bad;              // nullable
+  uint64_t n;
+};
+
+struct SnapEncArgs {
+  const uint8_t* base;
+  const uint64_t* offsets;      // raw block i = base[offsets[i], offsets[i+1])
+  uint8_t* out;
+  const uint64_t* out_offsets;  // compressed i starts at out + out_offsets[i]
+  uint64_t* out_len;            // compressed size (UINT64_MAX: block >= 2^32 bytes)
+  uint16_t* scratch;            // gridDim.x * kSnapMaxTable entries (large fragments)
+  uint64_t n;
+};
+
+}  // namespace lsbm

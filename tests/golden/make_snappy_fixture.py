@@ -20,7 +20,7 @@ import sys
 import pyarrow as pa
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from snappy_inputs import KINDS, block, varint32  # noqa: E402
+from snappy_inputs import KINDS, block, mutations, varint32  # noqa: E402
 
 CODEC = pa.Codec("snappy")
 
@@ -50,19 +50,6 @@ def uncompress(c):
 
 def sha(b):
     return hashlib.sha256(b).hexdigest()
-
-
-def mutations(c, seed):
-    """Deterministic corruptions of compressed block c: (name, bytes)."""
-    import numpy as np
-    rng = np.random.default_rng(seed)
-    out = [("truncate_1", c[:-1]), ("truncate_half", c[: len(c) // 2]), ("append_zero", c + b"\0"),
-           ("append_literal", c + b"\x00A")]
-    for j in range(4):
-        p = int(rng.integers(0, len(c)))
-        v = int(rng.integers(0, 256))
-        out.append(("set_%d_%d" % (p, v), c[:p] + bytes([v]) + c[p + 1:]))
-    return out
 
 
 def main():

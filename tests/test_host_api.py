@@ -22,7 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     """Every C function the C-ABI headers (include/lsbm_*.h) declare."""
     names = set()
-    for h in ("lsbm_crc32c.h", "lsbm_bloom.h"):
+    for h in ("lsbm_crc32c.h", "lsbm_bloom.h", "lsbm_snappy.h"):
         text = open(os.path.join(REPO, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names |= set(re.findall(r"\b(lsbm_\w+)\s*\(", text))
