@@ -17,6 +17,7 @@ namespace lsbm {
 // launchers (snappy_kernels.hip)
 hipError_t launch_snappy_length(const SnapLenArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream);
 
 namespace {
@@ -100,9 +101,13 @@ __attribute__((visibility("default"))) int lsbm_snappy_uncompress_dev(
   a.ok = d_ok;
   a.n_bad = d_n_bad;
   a.n = n;
-  const hipError_t e = launch_snappy_uncompress(a, wave_grid(cus, n, kSnapDecWgsPerCu),
-                                                static_cast<hipStream_t>(stream));
-  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_uncompress_kernel");
+  // pass 1: blocks that fit a small LDS slice; pass 2: the ones it deferred
+  // (ok = 2), scanned 64 per wave
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = launch_snappy_uncompress(a, wave_grid(cus, n, kSnapDecWgsPerCu), s);
+  if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_kernel");
+  e = launch_snappy_uncompress_large(a, wave_grid(cus, (n + 63) / 64, kSnapDecLargeWgsPerCu), s);
+  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_uncompress_large_kernel");
 }
 
 }  // extern "C"

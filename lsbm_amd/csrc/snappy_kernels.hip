@@ -39,6 +39,12 @@ __device__ __forceinline__ void wave_phase() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Compiler-only ordering for one wave's own LDS accesses (which the LDS
+// executes in issue order): emits no wait.
+__device__ __forceinline__ void wave_order() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
 // 8 bytes from p[i] on: LDS reads are two aligned dwords (the staged copy is
@@ -96,8 +102,11 @@ template <bool kLds>
 __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
   uint32_t ip = 0, op = 0;
   uint32_t fenced = 0;  // global variant: out[0, fenced) is visible to every lane
+  // The input is read-only, so the next tag's word is requested before the
+  // current tag's bytes move: the two LDS round trips overlap, and a tag costs
+  // one wait instead of three.
+  uint64_t w = ip < cl ? uni64(load8<kLds>(in, ip, cl)) : 0;
   while (ip < cl) {
-    const uint64_t w = uni64(load8<kLds>(in, ip, cl));
     const uint32_t c = (uint32_t)w & 0xffu;
     if ((c & 3u) == 0) {  // literal
       uint64_t len = (c >> 2) + 1;
@@ -112,9 +121,12 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
       if (len > (uint64_t)(cl - ip - hdr) || len > (uint64_t)(ulen - op)) return false;
       const uint8_t* src = in + ip + hdr;
       uint8_t* dst = out + op;
+      const uint32_t nip = ip + hdr + (uint32_t)len;
+      const uint64_t wn = nip < cl ? load8<kLds>(in, nip, cl) : 0;
       for (uint32_t j = lane; j < (uint32_t)len; j += 64) dst[j] = src[j];
-      ip += hdr + (uint32_t)len;
+      ip = nip;
       op += (uint32_t)len;
+      w = uni64(wn);
     } else {  // copy
       uint32_t hdr, len, off;
       const uint32_t kind = c & 3u;
@@ -136,55 +148,91 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
         wave_phase();
         fenced = op;
       }
+      const uint32_t nip = ip + hdr;
+      const uint64_t wn = nip < cl ? load8<kLds>(in, nip, cl) : 0;
       // byte j of the copy is out[op - off + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it.
       if (lane < len) {
         const uint32_t k = off >= len ? lane : lane % off;
         out[op + lane] = out[op - off + k];
       }
-      ip += hdr;
+      ip = nip;
       op += len;
+      w = uni64(wn);
     }
-    if (kLds) wave_phase();
+    // LDS variant: one wave's LDS accesses execute in issue order, so a copy
+    // reads the bytes earlier tags wrote without waiting for the writes; the
+    // wavefront-scope fence only keeps the compiler from reordering them.
+    if (kLds) wave_order();
   }
   return op == ulen;
 }
 
+// Decodes block b with the wave's LDS slice of kSlice bytes when its
+// compressed bytes and output fit, else (kGlobalFallback) against global
+// memory.  Returns 2 when the block neither fits nor may fall back.
+template <uint32_t kSlice, bool kGlobalFallback>
+__device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint64_t b, uint32_t lane) {
+  uint8_t* const lds_in = smem;
+  const uint64_t s = a.offsets[b], e = a.offsets[b + 1];
+  const uint64_t os = a.out_offsets[b], cap = a.out_offsets[b + 1] - os;
+  const uint64_t clen = e - s;
+  uint32_t ulen = 0;
+  const uint32_t pre = uni(parse_preamble(a.base + s, clen, &ulen));
+  ulen = uni(ulen);
+  if (pre == 0 || (uint64_t)ulen > cap) return 0;
+  const uint64_t cl64 = clen - pre;
+  const uint32_t cl_pad = (uint32_t)((cl64 + 8 + 15) & ~15ull);
+  bool ok;
+  if (cl64 + 8 + 15 + (uint64_t)ulen <= kSlice) {
+    const uint8_t* g = a.base + s + pre;
+    const uint32_t cl = (uint32_t)cl64;
+    for (uint32_t j = lane; j < cl + 8; j += 64) lds_in[j] = j < cl ? g[j] : 0;
+    uint8_t* win = smem + cl_pad;
+    wave_phase();
+    ok = decode<true>(lds_in, cl, win, ulen, lane);
+    if (ok) {
+      uint8_t* dst = a.out + os;
+      for (uint32_t j = lane; j < ulen; j += 64) dst[j] = win[j];
+    }
+    wave_phase();
+  } else if (!kGlobalFallback) {
+    return 2;
+  } else if (cl64 < 0xffffffffull) {
+    ok = decode<false>(a.base + s + pre, (uint32_t)cl64, a.out + os, ulen, lane);
+  } else {
+    ok = false;  // a >= 4 GiB compressed block (snappy's lengths are 32-bit)
+  }
+  return ok ? 1 : 0;
+}
+
+__device__ __forceinline__ void record(const SnapDecArgs& a, uint64_t b, uint32_t r, uint32_t lane) {
+  if (lane == 0) {
+    a.ok[b] = (uint8_t)r;
+    if (r == 0 && a.n_bad) atomicAdd(a.n_bad, 1u);
+  }
+}
+
+// Pass 1: every block that fits a small slice (a db_bench data block and its
+// compressed form need < 8 KiB), at kSnapDecWgsPerCu waves per CU; the rest
+// are marked ok = 2 for pass 2.
 __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_kernel(SnapDecArgs a) {
   const uint32_t lane = threadIdx.x;
-  uint8_t* const lds_in = smem;
-  for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x) {
-    const uint64_t s = a.offsets[b], e = a.offsets[b + 1];
-    const uint64_t os = a.out_offsets[b], cap = a.out_offsets[b + 1] - os;
-    const uint64_t clen = e - s;
-    uint32_t ulen = 0;
-    const uint32_t pre = uni(parse_preamble(a.base + s, clen, &ulen));
-    ulen = uni(ulen);
-    bool ok = pre != 0 && (uint64_t)ulen <= cap;
-    if (ok) {
-      const uint64_t cl64 = clen - pre;
-      const uint32_t cl_pad = (uint32_t)((cl64 + 8 + 15) & ~15ull);
-      if (cl64 + 8 + 15 + (uint64_t)ulen <= kSnapDecLds) {
-        const uint8_t* g = a.base + s + pre;
-        const uint32_t cl = (uint32_t)cl64;
-        for (uint32_t j = lane; j < cl + 8; j += 64) lds_in[j] = j < cl ? g[j] : 0;
-        uint8_t* win = smem + cl_pad;
-        wave_phase();
-        ok = decode<true>(lds_in, cl, win, ulen, lane);
-        if (ok) {
-          uint8_t* dst = a.out + os;
-          for (uint32_t j = lane; j < ulen; j += 64) dst[j] = win[j];
-        }
-        wave_phase();
-      } else if (cl64 < 0xffffffffull) {
-        ok = decode<false>(a.base + s + pre, (uint32_t)cl64, a.out + os, ulen, lane);
-      } else {
-        ok = false;  // a >= 4 GiB compressed block (snappy's lengths are 32-bit)
-      }
-    }
-    if (lane == 0) {
-      a.ok[b] = ok ? 1 : 0;
-      if (!ok && a.n_bad) atomicAdd(a.n_bad, 1u);
+  for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x)
+    record(a, b, uncompress_block<kSnapDecLds, false>(a, b, lane), lane);
+}
+
+// Pass 2: the blocks pass 1 deferred, found 64 at a time by ballot, in a
+// large slice or against global memory.
+__global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_large_kernel(SnapDecArgs a) {
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+    const uint64_t i = c + lane;
+    uint64_t pend = __ballot(i < a.n && a.ok[i] == 2);
+    while (pend) {
+      const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      record(a, b, uncompress_block<kSnapDecLdsLarge, true>(a, b, lane), lane);
     }
   }
 }
@@ -274,30 +322,76 @@ __device__ __forceinline__ uint32_t match_len(const uint8_t* in, uint32_t a, uin
 
 // snappy.cc CompressFragment over in[0, n) (n <= 64 KiB) with a zeroed table
 // of tsize entries; the walk mirrors oracle/snappy_oracle.c compress_fragment.
+// Lane k's probe of a match search whose first probe is at p with skip sc:
+// probe k+1 = probe k + (skip_k >> 5), skip_{k+1} = skip_k + (skip_k >> 5).
+__device__ __forceinline__ void probe_positions(uint32_t p, uint32_t sc, uint32_t lane, uint32_t* pk,
+                                                uint32_t* sk) {
+  for (uint32_t j = 0; j < 64; j++) {
+    if (lane == j) {
+      *pk = p;
+      *sk = sc;
+    }
+    const uint32_t st = sc >> 5;
+    p += st;
+    sc += st;
+  }
+}
+
 template <bool kLds>
 __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, uint32_t tsize,
-                                      uint8_t* out, uint64_t op, uint32_t lane) {
+                                      uint8_t* out, uint64_t op, uint32_t lane, uint32_t off32,
+                                      uint32_t sk32) {
   const uint32_t mask = tsize - 1;
   uint32_t ip = 0, next_emit = 0;
   if (n >= 15) {
     const uint32_t limit = n - 15;
     for (;;) {
       next_emit = ip++;
-      uint32_t skip = 32, cand;
+      uint32_t cand;
+      // The search's probe positions depend only on where it starts (skip
+      // restarts at 32), so the wave makes 64 probes at once, lane k taking
+      // probe k.  What the serial walk's table read would return for probe k
+      // is the position of the latest earlier lane with the same hash, if any,
+      // else the table's value; the first lane whose candidate matches is the
+      // serial walk's match, and lanes up to it update the table (the last
+      // writer of each hash only).
+      uint32_t pk = ip + off32, sk = sk32;
       for (;;) {
-        const uint32_t data = uni(load32<kLds>(in, ip));
+        const uint32_t step = sk >> 5;
+        const bool valid = pk + step <= limit;
+        const uint32_t data = load32<kLds>(in, valid ? pk : 0);
         const uint32_t h = hash_bytes(data, mask);
-        const uint32_t step = skip >> 5;
-        skip += step;
-        const uint32_t next_ip = ip + step;
-        if (next_ip > limit) {
+        const uint32_t old = table[h];
+        uint32_t pred = 64, succ = 64;
+        for (uint32_t j = 0; j < 64; j++) {
+          const uint32_t hj = __builtin_amdgcn_readlane(h, j);
+          if (hj == h) {
+            if (j < lane) pred = j;
+            else if (j > lane && succ == 64) succ = j;
+          }
+        }
+        const uint32_t ppos = (uint32_t)__shfl((int)pk, pred < 64 ? (int)pred : (int)lane);
+        const uint32_t c = pred < 64 ? ppos : old;
+        const bool m = valid && load32<kLds>(in, valid ? c : 0) == data;
+        const uint64_t mm = __ballot(m);
+        const uint64_t vm = __ballot(valid);
+        if (mm == 0 && vm != ~0ull) {  // the search reached the limit
           ip = next_emit;
           goto remainder;
         }
-        cand = uni(table[h]);
-        table[h] = (uint16_t)ip;
-        if (uni(load32<kLds>(in, cand)) == data) break;
-        ip = next_ip;
+        const uint32_t last = mm ? (uint32_t)__builtin_ctzll(mm) : 63u;
+        if (lane <= last && succ > last) table[h] = (uint16_t)pk;
+        // later reads of these entries come from other lanes: in LDS the
+        // wave's accesses run in order; in global memory wait for the stores
+        if (kLds) wave_order();
+        else wave_phase();
+        if (mm) {
+          ip = __builtin_amdgcn_readlane(pk, last);
+          cand = __builtin_amdgcn_readlane(c, last);
+          break;
+        }
+        const uint32_t p63 = __builtin_amdgcn_readlane(pk, 63), s63 = __builtin_amdgcn_readlane(sk, 63);
+        probe_positions(p63 + (s63 >> 5), s63 + (s63 >> 5), lane, &pk, &sk);
       }
       op = emit_literal(out, op, in + next_emit, ip - next_emit, lane);
       for (;;) {
@@ -324,6 +418,8 @@ remainder:
 __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncArgs a) {
   const uint32_t lane = threadIdx.x;
   uint16_t* const gtable = a.scratch + (uint64_t)blockIdx.x * kSnapMaxTable;
+  uint32_t off32 = 0, sk32 = 0;  // lane k's probe of a search from position 0, skip 32
+  probe_positions(0, 32, lane, &off32, &sk32);
   for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x) {
     const uint64_t s = a.offsets[b];
     const uint64_t len = a.offsets[b + 1] - s;
@@ -348,12 +444,12 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
         for (uint32_t j = lane; j < tsize / 2; j += 64) reinterpret_cast<uint32_t*>(smem)[j] = 0;
         for (uint32_t j = lane; j < fn; j += 64) lin[j] = g[j];
         wave_phase();
-        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane);
+        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32);
         wave_phase();
       } else {
         for (uint32_t j = lane; j < tsize; j += 64) gtable[j] = 0;
         wave_phase();
-        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane);
+        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32);
         wave_phase();
       }
     }
@@ -371,6 +467,12 @@ hipError_t launch_snappy_length(const SnapLenArgs& a, int grid, hipStream_t stre
 
 hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(grid), dim3(kSnapThreads), kSnapDecLds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(snappy_uncompress_large_kernel, dim3(grid), dim3(kSnapThreads), kSnapDecLdsLarge,
+                     stream, a);
   return hipGetLastError();
 }
 

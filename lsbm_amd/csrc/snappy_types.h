@@ -10,12 +10,16 @@ namespace lsbm {
 // algorithm against global memory (output, and the encoder's hash table in a
 // per-workgroup scratch slice).
 constexpr uint32_t kSnapThreads = 64;
-constexpr uint32_t kSnapDecLds = 16384;  // decoder: compressed bytes + 8 pad + output window
+// decoder slices hold the compressed bytes + 8 pad + the output window: pass 1
+// uses small slices (more waves in flight), pass 2 large ones
+constexpr uint32_t kSnapDecLds = 8192;
+constexpr uint32_t kSnapDecLdsLarge = 16384;
 constexpr uint32_t kSnapEncLds = 24576;  // encoder: hash table (2 B/entry) + fragment bytes
 constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
 constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
 constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
 constexpr uint32_t kSnapDecWgsPerCu = 160 * 1024 / kSnapDecLds;  // LDS-limited residency
+constexpr uint32_t kSnapDecLargeWgsPerCu = 160 * 1024 / kSnapDecLdsLarge;
 constexpr uint32_t kSnapEncWgsPerCu = 160 * 1024 / kSnapEncLds;
 
 struct SnapLenArgs {
