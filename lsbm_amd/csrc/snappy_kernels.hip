@@ -45,6 +45,49 @@ __device__ __forceinline__ void wave_order() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// dst[0, n) = g[0, n) for a 4-aligned LDS dst and any global g: aligned
+// dword loads (none past the dword holding g[n-1]), funnel-shifted into place,
+// 4 per lane in flight.  The last dword's bytes past n are unspecified.
+__device__ __forceinline__ void stage_to_lds(uint8_t* dst, const uint8_t* g, uint32_t n, uint32_t lane) {
+  const uintptr_t ga = reinterpret_cast<uintptr_t>(g);
+  const uint32_t sh = (uint32_t)(ga & 3u);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(ga - sh);
+  const uint32_t nsrc = (sh + n + 3) >> 2;
+  const uint32_t ndst = (n + 3) >> 2;
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (uint32_t k0 = 0; k0 < ndst; k0 += 256) {
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t k = k0 + u * 64 + lane;
+      lo[u] = k < nsrc ? src[k] : 0u;
+      hi[u] = k + 1 < nsrc ? src[k + 1] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t k = k0 + u * 64 + lane;
+      if (k < ndst) d[k] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh);
+    }
+  }
+}
+
+// g[0, n) = src[0, n) from LDS: 8 byte reads per lane issued before their stores.
+__device__ __forceinline__ void unstage_from_lds(uint8_t* g, const uint8_t* src, uint32_t n, uint32_t lane) {
+  for (uint32_t j0 = 0; j0 < n; j0 += 512) {
+    uint8_t v[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t j = j0 + u * 64 + lane;
+      v[u] = j < n ? src[j] : 0;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t j = j0 + u * 64 + lane;
+      if (j < n) g[j] = v[u];
+    }
+  }
+}
+
 extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
 // 8 bytes from p[i] on: LDS reads are two aligned dwords (the staged copy is
@@ -187,14 +230,13 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
   if (cl64 + 8 + 15 + (uint64_t)ulen <= kSlice) {
     const uint8_t* g = a.base + s + pre;
     const uint32_t cl = (uint32_t)cl64;
-    for (uint32_t j = lane; j < cl + 8; j += 64) lds_in[j] = j < cl ? g[j] : 0;
+    stage_to_lds(lds_in, g, cl, lane);
+    wave_order();
+    if (lane < 8) lds_in[cl + lane] = 0;  // zero pad behind the stream (load8 reads <= cl+6)
     uint8_t* win = smem + cl_pad;
     wave_phase();
     ok = decode<true>(lds_in, cl, win, ulen, lane);
-    if (ok) {
-      uint8_t* dst = a.out + os;
-      for (uint32_t j = lane; j < ulen; j += 64) dst[j] = win[j];
-    }
+    if (ok) unstage_from_lds(a.out + os, win, ulen, lane);
     wave_phase();
   } else if (!kGlobalFallback) {
     return 2;
@@ -340,7 +382,7 @@ __device__ __forceinline__ void probe_positions(uint32_t p, uint32_t sc, uint32_
 template <bool kLds>
 __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, uint32_t tsize,
                                       uint8_t* out, uint64_t op, uint32_t lane, uint32_t off32,
-                                      uint32_t sk32) {
+                                      uint32_t sk32, uint32_t* buckets) {
   const uint32_t mask = tsize - 1;
   uint32_t ip = 0, next_emit = 0;
   if (n >= 15) {
@@ -362,8 +404,18 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
         const uint32_t data = load32<kLds>(in, valid ? pk : 0);
         const uint32_t h = hash_bytes(data, mask);
         const uint32_t old = table[h];
+        // Lanes sharing a hash share one of kSnapEncBuckets LDS counters; only
+        // lanes whose counter reached 2 can have a same-hash peer, and the
+        // exact compare runs over those lanes alone (usually a few, not 64).
+        uint32_t* const cnt = buckets + (h & (kSnapEncBuckets - 1));
+        if (valid) atomicAdd(cnt, 1u);
+        const uint32_t nb = valid ? *cnt : 0u;
+        if (valid) *cnt = 0u;
+        uint64_t peers = __ballot(nb >= 2);
         uint32_t pred = 64, succ = 64;
-        for (uint32_t j = 0; j < 64; j++) {
+        while (peers) {
+          const uint32_t j = (uint32_t)__builtin_ctzll(peers);
+          peers &= peers - 1;
           const uint32_t hj = __builtin_amdgcn_readlane(h, j);
           if (hj == h) {
             if (j < lane) pred = j;
@@ -420,6 +472,11 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
   uint16_t* const gtable = a.scratch + (uint64_t)blockIdx.x * kSnapMaxTable;
   uint32_t off32 = 0, sk32 = 0;  // lane k's probe of a search from position 0, skip 32
   probe_positions(0, 32, lane, &off32, &sk32);
+  // hash-bucket counters of the batched search, behind the fragment's slice;
+  // zero between searches (every search clears what it counted)
+  uint32_t* const buckets = reinterpret_cast<uint32_t*>(smem + kSnapEncSlice);
+  for (uint32_t j = lane; j < kSnapEncBuckets; j += 64) buckets[j] = 0;
+  wave_order();
   for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x) {
     const uint64_t s = a.offsets[b];
     const uint64_t len = a.offsets[b + 1] - s;
@@ -438,18 +495,18 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
       const uint32_t fn = n - pos < kSnapFragment ? n - pos : kSnapFragment;
       const uint32_t tsize = table_size_for(fn);
       const uint8_t* g = a.base + s + pos;
-      if (2 * tsize + fn <= kSnapEncLds) {
+      if (2 * tsize + fn + 4 <= kSnapEncSlice) {  // + the staged copy's last dword
         uint16_t* table = reinterpret_cast<uint16_t*>(smem);
         uint8_t* lin = smem + 2 * tsize;
-        for (uint32_t j = lane; j < tsize / 2; j += 64) reinterpret_cast<uint32_t*>(smem)[j] = 0;
-        for (uint32_t j = lane; j < fn; j += 64) lin[j] = g[j];
+        for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
+        stage_to_lds(lin, g, fn, lane);
         wave_phase();
-        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32);
+        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, buckets);
         wave_phase();
       } else {
         for (uint32_t j = lane; j < tsize; j += 64) gtable[j] = 0;
         wave_phase();
-        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32);
+        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, buckets);
         wave_phase();
       }
     }

@@ -14,7 +14,11 @@ constexpr uint32_t kSnapThreads = 64;
 // uses small slices (more waves in flight), pass 2 large ones
 constexpr uint32_t kSnapDecLds = 8192;
 constexpr uint32_t kSnapDecLdsLarge = 16384;
-constexpr uint32_t kSnapEncLds = 24576;  // encoder: hash table (2 B/entry) + fragment bytes
+// encoder: hash table (2 B/entry) + fragment bytes in a 24 KiB slice, then
+// the match search's hash-bucket counters
+constexpr uint32_t kSnapEncSlice = 24576;
+constexpr uint32_t kSnapEncBuckets = 512;
+constexpr uint32_t kSnapEncLds = kSnapEncSlice + 4 * kSnapEncBuckets;
 constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
 constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
 constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
