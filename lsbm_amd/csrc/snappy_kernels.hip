@@ -405,33 +405,52 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
         const uint32_t h = hash_bytes(data, mask);
         const uint32_t old = table[h];
         // Lanes sharing a hash share one of kSnapEncBuckets LDS counters; only
-        // lanes whose counter reached 2 can have a same-hash peer, and the
-        // exact compare runs over those lanes alone (usually a few, not 64).
+        // lanes whose counter reached 2 can have a same-hash peer.
         uint32_t* const cnt = buckets + (h & (kSnapEncBuckets - 1));
         if (valid) atomicAdd(cnt, 1u);
         const uint32_t nb = valid ? *cnt : 0u;
         if (valid) *cnt = 0u;
-        uint64_t peers = __ballot(nb >= 2);
-        uint32_t pred = 64, succ = 64;
-        while (peers) {
-          const uint32_t j = (uint32_t)__builtin_ctzll(peers);
-          peers &= peers - 1;
+        const uint64_t flagged = __ballot(nb >= 2);
+        // a lane with no peer matches iff the table's candidate does
+        const bool m0 = valid && load32<kLds>(in, valid ? old : 0) == data;
+        const uint64_t vm = __ballot(valid);
+        const uint64_t mm0 = __ballot(m0) & ~flagged;
+        const uint32_t lnf = mm0 ? (uint32_t)__builtin_ctzll(mm0) : 64u;
+        // Flagged lanes in ascending order.  When the walk reaches lane j, j's
+        // latest same-hash predecessor is final, and with it j's candidate;
+        // a predecessor holds the same hash, so j matches iff their 4 bytes
+        // agree (data in registers, no load).  The walk stops at the first
+        // flagged match or past the first unflagged one: later lanes do not
+        // matter.  st: bit 0 = has a predecessor, bit 1 = its bytes agree.
+        uint32_t pred = 64, succ = 64, st = 0;
+        uint32_t last = lnf;
+        for (uint64_t f = flagged; f;) {
+          const uint32_t j = (uint32_t)__builtin_ctzll(f);
+          f &= f - 1;
+          if (j > lnf) break;
           const uint32_t hj = __builtin_amdgcn_readlane(h, j);
+          const uint32_t dj = __builtin_amdgcn_readlane(data, j);
+          const uint32_t sj = __builtin_amdgcn_readlane(st, j);
+          const bool mj = (sj & 1u) ? (sj & 2u) != 0 : __builtin_amdgcn_readlane((uint32_t)m0, j) != 0;
           if (hj == h) {
-            if (j < lane) pred = j;
-            else if (j > lane && succ == 64) succ = j;
+            if (j < lane) {
+              pred = j;
+              st = 1u | (dj == data ? 2u : 0u);
+            } else if (j > lane && succ == 64) {
+              succ = j;
+            }
+          }
+          if (mj) {
+            last = j;
+            break;
           }
         }
-        const uint32_t ppos = (uint32_t)__shfl((int)pk, pred < 64 ? (int)pred : (int)lane);
-        const uint32_t c = pred < 64 ? ppos : old;
-        const bool m = valid && load32<kLds>(in, valid ? c : 0) == data;
-        const uint64_t mm = __ballot(m);
-        const uint64_t vm = __ballot(valid);
-        if (mm == 0 && vm != ~0ull) {  // the search reached the limit
+        if (last == 64 && vm != ~0ull) {  // the search reached the limit
           ip = next_emit;
           goto remainder;
         }
-        const uint32_t last = mm ? (uint32_t)__builtin_ctzll(mm) : 63u;
+        const uint64_t mm = last < 64 ? 1ull : 0ull;
+        if (last == 64) last = 63;
         if (lane <= last && succ > last) table[h] = (uint16_t)pk;
         // later reads of these entries come from other lanes: in LDS the
         // wave's accesses run in order; in global memory wait for the stores
@@ -439,7 +458,8 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
         else wave_phase();
         if (mm) {
           ip = __builtin_amdgcn_readlane(pk, last);
-          cand = __builtin_amdgcn_readlane(c, last);
+          const uint32_t pl = __builtin_amdgcn_readlane(pred, last);
+          cand = pl < 64 ? __builtin_amdgcn_readlane(pk, pl) : __builtin_amdgcn_readlane(old, last);
           break;
         }
         const uint32_t p63 = __builtin_amdgcn_readlane(pk, 63), s63 = __builtin_amdgcn_readlane(sk, 63);
