@@ -90,6 +90,29 @@ __device__ __forceinline__ void unstage_from_lds(uint8_t* g, const uint8_t* src,
 
 extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
+// Phase timing of the encoder (diagnostic build only, -DLSBM_SNAP_STAMPS;
+// tools/snappy_stamps.py): s_memtime deltas per phase, summed per wave.
+#ifdef LSBM_SNAP_STAMPS
+__device__ unsigned long long g_snap_stamps[10];
+struct Stamps {
+  uint64_t t, acc[8];
+};
+#define SNAP_STAMP(k)                                    \
+  do {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+    sa.acc[k] += t_ - sa.t;                              \
+    sa.t = t_;                                           \
+  } while (0)
+#define SNAP_STAMPS_PARAM , Stamps& sa
+#define SNAP_STAMPS_ARG , sa
+#else
+#define SNAP_STAMP(k) \
+  do {                \
+  } while (0)
+#define SNAP_STAMPS_PARAM
+#define SNAP_STAMPS_ARG
+#endif
+
 // 8 bytes from p[i] on: LDS reads are two aligned dwords (the staged copy is
 // padded, so this never reads past the slice); global reads are bytes bounded
 // by n (zero past the end).
@@ -382,13 +405,14 @@ __device__ __forceinline__ void probe_positions(uint32_t p, uint32_t sc, uint32_
 template <bool kLds>
 __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, uint32_t tsize,
                                       uint8_t* out, uint64_t op, uint32_t lane, uint32_t off32,
-                                      uint32_t sk32, uint32_t* buckets) {
+                                      uint32_t sk32, uint32_t* buckets SNAP_STAMPS_PARAM) {
   const uint32_t mask = tsize - 1;
   uint32_t ip = 0, next_emit = 0;
   if (n >= 15) {
     const uint32_t limit = n - 15;
     for (;;) {
       next_emit = ip++;
+      SNAP_STAMP(4);
       uint32_t cand;
       // The search's probe positions depend only on where it starts (skip
       // restarts at 32), so the wave makes 64 probes at once, lane k taking
@@ -400,17 +424,21 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
       uint32_t pk = ip + off32, sk = sk32;
       for (;;) {
         const uint32_t step = sk >> 5;
-        const bool valid = pk + step <= limit;
+        const bool valid = lane < kSnapProbes && pk + step <= limit;
         const uint32_t data = load32<kLds>(in, valid ? pk : 0);
         const uint32_t h = hash_bytes(data, mask);
         const uint32_t old = table[h];
         // Lanes sharing a hash share one of kSnapEncBuckets LDS counters; only
         // lanes whose counter reached 2 can have a same-hash peer.
-        uint32_t* const cnt = buckets + (h & (kSnapEncBuckets - 1));
-        if (valid) atomicAdd(cnt, 1u);
-        const uint32_t nb = valid ? *cnt : 0u;
+        // (8-bit counters, four to a dword: a batch counts at most 64)
+        const uint32_t bk = h & (kSnapEncBuckets - 1);
+        uint32_t* const cnt = buckets + (bk >> 2);
+        const uint32_t bsh = 8 * (bk & 3u);
+        if (valid) atomicAdd(cnt, 1u << bsh);
+        const uint32_t nb = valid ? (*cnt >> bsh) & 0xffu : 0u;
         if (valid) *cnt = 0u;
         const uint64_t flagged = __ballot(nb >= 2);
+        SNAP_STAMP(6);
         // a lane with no peer matches iff the table's candidate does
         const bool m0 = valid && load32<kLds>(in, valid ? old : 0) == data;
         const uint64_t vm = __ballot(valid);
@@ -432,25 +460,25 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
           const uint32_t dj = __builtin_amdgcn_readlane(data, j);
           const uint32_t sj = __builtin_amdgcn_readlane(st, j);
           const bool mj = (sj & 1u) ? (sj & 2u) != 0 : __builtin_amdgcn_readlane((uint32_t)m0, j) != 0;
-          if (hj == h) {
-            if (j < lane) {
-              pred = j;
-              st = 1u | (dj == data ? 2u : 0u);
-            } else if (j > lane && succ == 64) {
-              succ = j;
-            }
-          }
+          // branch-free updates (selects, no divergent branches)
+          const bool eq = hj == h;
+          const bool after = eq && lane > j;
+          pred = after ? j : pred;
+          st = after ? (dj == data ? 3u : 1u) : st;
+          succ = (eq && lane < j && succ == 64) ? j : succ;
           if (mj) {
             last = j;
             break;
           }
         }
-        if (last == 64 && vm != ~0ull) {  // the search reached the limit
+        SNAP_STAMP(7);
+        constexpr uint64_t kAll = kSnapProbes == 64 ? ~0ull : (1ull << kSnapProbes) - 1;
+        if (last == 64 && vm != kAll) {  // the search reached the limit
           ip = next_emit;
           goto remainder;
         }
         const uint64_t mm = last < 64 ? 1ull : 0ull;
-        if (last == 64) last = 63;
+        if (last == 64) last = kSnapProbes - 1;
         if (lane <= last && succ > last) table[h] = (uint16_t)pk;
         // later reads of these entries come from other lanes: in LDS the
         // wave's accesses run in order; in global memory wait for the stores
@@ -462,15 +490,19 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
           cand = pl < 64 ? __builtin_amdgcn_readlane(pk, pl) : __builtin_amdgcn_readlane(old, last);
           break;
         }
-        const uint32_t p63 = __builtin_amdgcn_readlane(pk, 63), s63 = __builtin_amdgcn_readlane(sk, 63);
-        probe_positions(p63 + (s63 >> 5), s63 + (s63 >> 5), lane, &pk, &sk);
+        const uint32_t pl = __builtin_amdgcn_readlane(pk, kSnapProbes - 1);
+        const uint32_t sl = __builtin_amdgcn_readlane(sk, kSnapProbes - 1);
+        probe_positions(pl + (sl >> 5), sl + (sl >> 5), lane, &pk, &sk);
       }
+      SNAP_STAMP(1);
       op = emit_literal(out, op, in + next_emit, ip - next_emit, lane);
+      SNAP_STAMP(2);
       for (;;) {
         const uint32_t base = ip;
         const uint32_t matched = 4 + uni(match_len(in, cand + 4, ip + 4, n, lane));
         ip += matched;
         op = emit_copy(out, op, base - cand, matched, lane);
+        SNAP_STAMP(3);
         next_emit = ip;
         if (ip >= limit) goto remainder;
         table[hash_bytes(uni(load32<kLds>(in, ip - 1)), mask)] = (uint16_t)(ip - 1);
@@ -483,7 +515,9 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
     }
   }
 remainder:
+  SNAP_STAMP(4);
   if (next_emit < n) op = emit_literal(out, op, in + next_emit, n - next_emit, lane);
+  SNAP_STAMP(5);
   return op;
 }
 
@@ -495,8 +529,12 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
   // hash-bucket counters of the batched search, behind the fragment's slice;
   // zero between searches (every search clears what it counted)
   uint32_t* const buckets = reinterpret_cast<uint32_t*>(smem + kSnapEncSlice);
-  for (uint32_t j = lane; j < kSnapEncBuckets; j += 64) buckets[j] = 0;
+  for (uint32_t j = lane; j < kSnapEncBuckets / 4; j += 64) buckets[j] = 0;
   wave_order();
+#ifdef LSBM_SNAP_STAMPS
+  Stamps sa = {};
+  sa.t = __builtin_amdgcn_s_memtime();
+#endif
   for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x) {
     const uint64_t s = a.offsets[b];
     const uint64_t len = a.offsets[b + 1] - s;
@@ -521,17 +559,25 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
         for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
         stage_to_lds(lin, g, fn, lane);
         wave_phase();
-        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, buckets);
+        SNAP_STAMP(0);  // staging, table zeroing, preamble
+        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, buckets SNAP_STAMPS_ARG);
         wave_phase();
       } else {
         for (uint32_t j = lane; j < tsize; j += 64) gtable[j] = 0;
         wave_phase();
-        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, buckets);
+        SNAP_STAMP(0);
+        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, buckets SNAP_STAMPS_ARG);
         wave_phase();
       }
     }
     if (lane == 0) a.out_len[b] = op;
   }
+#ifdef LSBM_SNAP_STAMPS
+  if (lane == 0) {
+    for (int k = 0; k < 8; k++) atomicAdd(&g_snap_stamps[k], (unsigned long long)sa.acc[k]);
+    atomicAdd(&g_snap_stamps[9], 1ull);
+  }
+#endif
 }
 
 }  // namespace
@@ -559,3 +605,17 @@ hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t st
 }
 
 }  // namespace lsbm
+
+#ifdef LSBM_SNAP_STAMPS
+extern "C" __attribute__((visibility("default"))) int lsbm_snappy_debug_stamps(unsigned long long* out10,
+                                                                                int reset) {
+  if (hipMemcpyFromSymbol(out10, HIP_SYMBOL(lsbm::g_snap_stamps), 10 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[10] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lsbm::g_snap_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -15,10 +15,14 @@ constexpr uint32_t kSnapThreads = 64;
 constexpr uint32_t kSnapDecLds = 8192;
 constexpr uint32_t kSnapDecLdsLarge = 16384;
 // encoder: hash table (2 B/entry) + fragment bytes in a 24 KiB slice, then
-// the match search's hash-bucket counters
+// the match search's hash-bucket counters (one byte each)
 constexpr uint32_t kSnapEncSlice = 24576;
-constexpr uint32_t kSnapEncBuckets = 512;
-constexpr uint32_t kSnapEncLds = kSnapEncSlice + 4 * kSnapEncBuckets;
+constexpr uint32_t kSnapEncBuckets = 2048;  // 8-bit counters
+#ifndef LSBM_SNAP_PROBES
+#define LSBM_SNAP_PROBES 32
+#endif
+constexpr uint32_t kSnapProbes = LSBM_SNAP_PROBES;  // match-search probes per wave step (<= 64)
+constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
 constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
 constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
 constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
