@@ -405,7 +405,8 @@ __device__ __forceinline__ void probe_positions(uint32_t p, uint32_t sc, uint32_
 template <bool kLds>
 __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, uint32_t tsize,
                                       uint8_t* out, uint64_t op, uint32_t lane, uint32_t off32,
-                                      uint32_t sk32, uint32_t* buckets SNAP_STAMPS_PARAM) {
+                                      uint32_t sk32, uint32_t off64, uint32_t sk64,
+                                      uint32_t* buckets SNAP_STAMPS_PARAM) {
   const uint32_t mask = tsize - 1;
   uint32_t ip = 0, next_emit = 0;
   if (n >= 15) {
@@ -421,6 +422,8 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
       // else the table's value; the first lane whose candidate matches is the
       // serial walk's match, and lanes up to it update the table (the last
       // writer of each hash only).
+      const uint32_t start = ip;
+      uint32_t k0 = 0;
       uint32_t pk = ip + off32, sk = sk32;
       for (;;) {
         const uint32_t step = sk >> 5;
@@ -490,9 +493,22 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
           cand = pl < 64 ? __builtin_amdgcn_readlane(pk, pl) : __builtin_amdgcn_readlane(old, last);
           break;
         }
-        const uint32_t pl = __builtin_amdgcn_readlane(pk, kSnapProbes - 1);
-        const uint32_t sl = __builtin_amdgcn_readlane(sk, kSnapProbes - 1);
-        probe_positions(pl + (sl >> 5), sl + (sl >> 5), lane, &pk, &sk);
+        // next step: probes k0 + lane of the search, from the per-wave tables
+        // of the first 128 (a search's probe offsets do not depend on where
+        // it starts), else by the serial recurrence
+        k0 += kSnapProbes;
+        if (k0 + 64 <= 128) {
+          const int src = (int)((k0 + lane) & 63u);
+          const uint32_t oa = (uint32_t)__shfl((int)off32, src), ob = (uint32_t)__shfl((int)off64, src);
+          const uint32_t sa = (uint32_t)__shfl((int)sk32, src), sb = (uint32_t)__shfl((int)sk64, src);
+          const bool hi = k0 + lane >= 64;
+          pk = start + (hi ? ob : oa);
+          sk = hi ? sb : sa;
+        } else {
+          const uint32_t pl = __builtin_amdgcn_readlane(pk, kSnapProbes - 1);
+          const uint32_t sl = __builtin_amdgcn_readlane(sk, kSnapProbes - 1);
+          probe_positions(pl + (sl >> 5), sl + (sl >> 5), lane, &pk, &sk);
+        }
       }
       SNAP_STAMP(1);
       op = emit_literal(out, op, in + next_emit, ip - next_emit, lane);
@@ -524,8 +540,13 @@ remainder:
 __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncArgs a) {
   const uint32_t lane = threadIdx.x;
   uint16_t* const gtable = a.scratch + (uint64_t)blockIdx.x * kSnapMaxTable;
-  uint32_t off32 = 0, sk32 = 0;  // lane k's probe of a search from position 0, skip 32
+  // probes k = lane and k = 64 + lane of a search from position 0, skip 32
+  uint32_t off32 = 0, sk32 = 0, off64 = 0, sk64 = 0;
   probe_positions(0, 32, lane, &off32, &sk32);
+  {
+    const uint32_t p63 = __builtin_amdgcn_readlane(off32, 63), s63 = __builtin_amdgcn_readlane(sk32, 63);
+    probe_positions(p63 + (s63 >> 5), s63 + (s63 >> 5), lane, &off64, &sk64);
+  }
   // hash-bucket counters of the batched search, behind the fragment's slice;
   // zero between searches (every search clears what it counted)
   uint32_t* const buckets = reinterpret_cast<uint32_t*>(smem + kSnapEncSlice);
@@ -560,13 +581,13 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
         stage_to_lds(lin, g, fn, lane);
         wave_phase();
         SNAP_STAMP(0);  // staging, table zeroing, preamble
-        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, buckets SNAP_STAMPS_ARG);
+        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, off64, sk64, buckets SNAP_STAMPS_ARG);
         wave_phase();
       } else {
         for (uint32_t j = lane; j < tsize; j += 64) gtable[j] = 0;
         wave_phase();
         SNAP_STAMP(0);
-        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, buckets SNAP_STAMPS_ARG);
+        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, off64, sk64, buckets SNAP_STAMPS_ARG);
         wave_phase();
       }
     }
