@@ -497,7 +497,7 @@ __device__ uint64_t compress_fragment(const uint8_t* in, uint32_t n, uint16_t* t
         // of the first 128 (a search's probe offsets do not depend on where
         // it starts), else by the serial recurrence
         k0 += kSnapProbes;
-        if (k0 + 64 <= 128) {
+        if (k0 + kSnapProbes <= 128) {
           const int src = (int)((k0 + lane) & 63u);
           const uint32_t oa = (uint32_t)__shfl((int)off32, src), ob = (uint32_t)__shfl((int)off64, src);
           const uint32_t sa = (uint32_t)__shfl((int)sk32, src), sb = (uint32_t)__shfl((int)sk64, src);

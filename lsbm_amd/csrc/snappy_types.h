@@ -19,7 +19,7 @@ constexpr uint32_t kSnapDecLdsLarge = 16384;
 constexpr uint32_t kSnapEncSlice = 24576;
 constexpr uint32_t kSnapEncBuckets = 2048;  // 8-bit counters
 #ifndef LSBM_SNAP_PROBES
-#define LSBM_SNAP_PROBES 32
+#define LSBM_SNAP_PROBES 16
 #endif
 constexpr uint32_t kSnapProbes = LSBM_SNAP_PROBES;  // match-search probes per wave step (<= 64)
 constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
