@@ -14,15 +14,16 @@ constexpr uint32_t kSnapThreads = 64;
 // uses small slices (more waves in flight), pass 2 large ones
 constexpr uint32_t kSnapDecLds = 8192;
 constexpr uint32_t kSnapDecLdsLarge = 16384;
-// encoder: hash table (2 B/entry) + fragment bytes in a 24 KiB slice, then
-// the match search's hash-bucket counters (one byte each)
-constexpr uint32_t kSnapEncSlice = 24576;
-constexpr uint32_t kSnapEncBuckets = 2048;  // 8-bit counters
+// encoder: hash table (2 B/entry) + fragment bytes in a 22 KiB slice (a
+// 4 KiB block with its 8,192-entry table needs 20.1 KiB), then the match
+// search's hash-bucket counters (one byte each): 22.5 KiB, 7 waves per CU
+constexpr uint32_t kSnapEncSlice = 22528;
+constexpr uint32_t kSnapEncBuckets = 512;
+constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
 #ifndef LSBM_SNAP_PROBES
 #define LSBM_SNAP_PROBES 16
 #endif
 constexpr uint32_t kSnapProbes = LSBM_SNAP_PROBES;  // match-search probes per wave step (<= 64)
-constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
 constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
 constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
 constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
