@@ -268,6 +268,25 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     assert r.stdout.startswith("OK")
 
 
+def test_cpp_block_compression_layer(torch_cuda, tmp_path):
+    """include/lsbm/block_compression.h from C++: WriteBlock's compression and
+    12.5% rule against the snappy oracle, ReadBlock's decompression and its
+    Corruption statuses, then SealBlocks / VerifyBlocks over the result."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "compression_gpu_test"
+    libdir = os.path.join(repo, "lsbm_amd")
+    odir = os.path.join(repo, "oracle")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(repo, "include"),
+                    os.path.join(repo, "tests", "cpp", "compression_gpu_test.cc"), "-L", libdir,
+                    "-llsbm_crc32c", "-L", odir, "-loracle_snappy",
+                    "-Wl,-rpath," + libdir + ":" + odir, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK")
+
+
 def test_host_staged_pinned_source_and_chunking(torch_cuda, oracle):
     """A page-locked source is DMA-ed directly (no gather); > 64 MiB spans chunks."""
     torch = torch_cuda
