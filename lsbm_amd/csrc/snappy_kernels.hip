@@ -71,21 +71,27 @@ __device__ __forceinline__ void stage_to_lds(uint8_t* dst, const uint8_t* g, uin
   }
 }
 
-// g[0, n) = src[0, n) from LDS: 8 byte reads per lane issued before their stores.
+// g[0, n) = src[0, n) from a 16-aligned LDS src: byte stores up to g's next
+// 16-byte boundary, then 16-byte stores (five aligned LDS dwords per lane,
+// funnel-shifted), then the < 16-byte tail.  Byte-wide global stores of a
+// whole block cost a third of the decoder's time.
 __device__ __forceinline__ void unstage_from_lds(uint8_t* g, const uint8_t* src, uint32_t n, uint32_t lane) {
-  for (uint32_t j0 = 0; j0 < n; j0 += 512) {
-    uint8_t v[8];
-#pragma unroll
-    for (uint32_t u = 0; u < 8; u++) {
-      const uint32_t j = j0 + u * 64 + lane;
-      v[u] = j < n ? src[j] : 0;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < 8; u++) {
-      const uint32_t j = j0 + u * 64 + lane;
-      if (j < n) g[j] = v[u];
-    }
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+  const uint32_t head = min(n, (16u - mis) & 15u);
+  if (lane < head) g[lane] = src[lane];
+  const uint32_t nq = (n - head) >> 4;
+  const uint32_t sh = head & 3u;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(src + (head & ~3u));
+  uint4* gd = reinterpret_cast<uint4*>(g + head);
+  for (uint32_t q = lane; q < nq; q += 64) {
+    const uint32_t* p = w + 4 * q;
+    const uint32_t x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+    const uint32_t x4 = sh ? p[4] : 0u;  // holds needed bytes only when shifted
+    gd[q] = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
   }
+  const uint32_t t = head + 16 * nq + lane;
+  if (t < n) g[t] = src[t];
 }
 
 extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -93,7 +99,7 @@ extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 // Phase timing of the encoder (diagnostic build only, -DLSBM_SNAP_STAMPS;
 // tools/snappy_stamps.py): s_memtime deltas per phase, summed per wave.
 #ifdef LSBM_SNAP_STAMPS
-__device__ unsigned long long g_snap_stamps[10];
+__device__ unsigned long long g_snap_stamps[16];  // 0-7 encoder phases, 9 encoder waves, 10-13 decoder, 15 decoder waves
 struct Stamps {
   uint64_t t, acc[8];
 };
@@ -238,7 +244,8 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 // compressed bytes and output fit, else (kGlobalFallback) against global
 // memory.  Returns 2 when the block neither fits nor may fall back.
 template <uint32_t kSlice, bool kGlobalFallback>
-__device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint64_t b, uint32_t lane) {
+__device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint64_t b, uint32_t lane
+                                                     SNAP_STAMPS_PARAM) {
   uint8_t* const lds_in = smem;
   const uint64_t s = a.offsets[b], e = a.offsets[b + 1];
   const uint64_t os = a.out_offsets[b], cap = a.out_offsets[b + 1] - os;
@@ -253,13 +260,17 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
   if (cl64 + 8 + 15 + (uint64_t)ulen <= kSlice) {
     const uint8_t* g = a.base + s + pre;
     const uint32_t cl = (uint32_t)cl64;
+    SNAP_STAMP(0);  // offsets + preamble
     stage_to_lds(lds_in, g, cl, lane);
     wave_order();
     if (lane < 8) lds_in[cl + lane] = 0;  // zero pad behind the stream (load8 reads <= cl+6)
     uint8_t* win = smem + cl_pad;
     wave_phase();
+    SNAP_STAMP(1);
     ok = decode<true>(lds_in, cl, win, ulen, lane);
+    SNAP_STAMP(2);
     if (ok) unstage_from_lds(a.out + os, win, ulen, lane);
+    SNAP_STAMP(3);
     wave_phase();
   } else if (!kGlobalFallback) {
     return 2;
@@ -283,8 +294,18 @@ __device__ __forceinline__ void record(const SnapDecArgs& a, uint64_t b, uint32_
 // are marked ok = 2 for pass 2.
 __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_kernel(SnapDecArgs a) {
   const uint32_t lane = threadIdx.x;
+#ifdef LSBM_SNAP_STAMPS
+  Stamps sa = {};
+  sa.t = __builtin_amdgcn_s_memtime();
+#endif
   for (uint64_t b = blockIdx.x; b < a.n; b += gridDim.x)
-    record(a, b, uncompress_block<kSnapDecLds, false>(a, b, lane), lane);
+    record(a, b, uncompress_block<kSnapDecLds, false>(a, b, lane SNAP_STAMPS_ARG), lane);
+#ifdef LSBM_SNAP_STAMPS
+  if (lane == 0) {
+    for (int k = 0; k < 4; k++) atomicAdd(&g_snap_stamps[10 + k], (unsigned long long)sa.acc[k]);
+    atomicAdd(&g_snap_stamps[15], 1ull);
+  }
+#endif
 }
 
 // Pass 2: the blocks pass 1 deferred, found 64 at a time by ballot, in a
@@ -297,7 +318,10 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_large_kernel(S
     while (pend) {
       const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
       pend &= pend - 1;
-      record(a, b, uncompress_block<kSnapDecLdsLarge, true>(a, b, lane), lane);
+#ifdef LSBM_SNAP_STAMPS
+      Stamps sa = {};
+#endif
+      record(a, b, uncompress_block<kSnapDecLdsLarge, true>(a, b, lane SNAP_STAMPS_ARG), lane);
     }
   }
 }
@@ -628,13 +652,13 @@ hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t st
 }  // namespace lsbm
 
 #ifdef LSBM_SNAP_STAMPS
-extern "C" __attribute__((visibility("default"))) int lsbm_snappy_debug_stamps(unsigned long long* out10,
+extern "C" __attribute__((visibility("default"))) int lsbm_snappy_debug_stamps(unsigned long long* out16,
                                                                                 int reset) {
-  if (hipMemcpyFromSymbol(out10, HIP_SYMBOL(lsbm::g_snap_stamps), 10 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lsbm::g_snap_stamps), 16 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
   if (reset) {
-    unsigned long long z[10] = {};
+    unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lsbm::g_snap_stamps), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -26,7 +26,7 @@ o = torch.from_numpy(offs).cuda()
 oo = torch.from_numpy(ooffs).cuda()
 out = torch.empty(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
 ol = torch.empty(len(blocks), dtype=torch.int64, device="cuda")
-st = (ctypes.c_ulonglong * 10)()
+st = (ctypes.c_ulonglong * 16)()
 for rep in range(3):
     L.lsbm_snappy_debug_stamps(st, 1)
     rc = L.lsbm_snappy_compress_dev(ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(o.data_ptr()),
@@ -41,3 +41,27 @@ for rep in range(3):
     tot = sum(st[k] for k in range(8))
     print("rep %d waves %d blocks %d  memtime ticks/block %.0f  " % (rep, st[9], nb, tot / nb) +
           "  ".join("%s %.0f (%.0f%%)" % (names[k], st[k] / nb, 100.0 * st[k] / tot) for k in range(8)))
+
+# decoder phases over the compressed blocks
+nc = ol.cpu().numpy()
+comp = out.cpu().numpy()
+cblocks = [comp[int(ooffs[i]):int(ooffs[i]) + int(nc[i])].tobytes() for i in range(len(blocks))]
+cdata = np.frombuffer(b"".join(cblocks), np.uint8)
+coffs = np.concatenate([[0], np.cumsum([len(c) for c in cblocks])]).astype(np.int64)
+cd = torch.from_numpy(cdata.copy()).cuda()
+co = torch.from_numpy(coffs).cuda()
+dout = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
+okd = torch.empty(len(blocks), dtype=torch.uint8, device="cuda")
+for rep in range(3):
+    L.lsbm_snappy_debug_stamps(st, 1)
+    rc = L.lsbm_snappy_uncompress_dev(ctypes.c_void_p(cd.data_ptr()), ctypes.c_void_p(co.data_ptr()),
+                                      ctypes.c_uint64(len(blocks)), ctypes.c_void_p(dout.data_ptr()),
+                                      ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(okd.data_ptr()), None, None)
+    torch.cuda.synchronize()
+    assert rc == 0, rc
+    assert bool((okd == 1).all()) and torch.equal(dout, d)
+    L.lsbm_snappy_debug_stamps(st, 0)
+    names = ["offsets+preamble", "stage", "decode", "unstage"]
+    tot = sum(st[10 + k] for k in range(4))
+    print("decode rep %d waves %d blocks %d  ticks/block %.0f  " % (rep, st[15], nb, tot / nb) +
+          "  ".join("%s %.0f (%.0f%%)" % (names[k], st[10 + k] / nb, 100.0 * st[10 + k] / tot) for k in range(4)))
