@@ -136,6 +136,26 @@ __device__ __forceinline__ uint64_t load8(const uint8_t* p, uint32_t i, uint32_t
   }
 }
 
+// load8 split in two, so that the two LDS dwords can be requested early and
+// combined only where the value is needed (the shift would otherwise wait for
+// the load right after issuing it).
+struct Raw8 {
+  uint64_t v;
+  uint32_t sh;
+};
+
+template <bool kLds>
+__device__ __forceinline__ Raw8 issue8(const uint8_t* p, uint32_t i, uint32_t n) {
+  if (kLds) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p + (i & ~3u));
+    return Raw8{(uint64_t)w[0] | ((uint64_t)w[1] << 32), 8 * (i & 3u)};
+  } else {
+    return Raw8{load8<false>(p, i, n), 0};
+  }
+}
+
+__device__ __forceinline__ uint64_t finish8(Raw8 r) { return r.v >> r.sh; }
+
 template <bool kLds>
 __device__ __forceinline__ uint32_t load32(const uint8_t* p, uint32_t i) {
   if (kLds) {
@@ -194,11 +214,11 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
       const uint8_t* src = in + ip + hdr;
       uint8_t* dst = out + op;
       const uint32_t nip = ip + hdr + (uint32_t)len;
-      const uint64_t wn = nip < cl ? load8<kLds>(in, nip, cl) : 0;
+      const Raw8 wn = nip < cl ? issue8<kLds>(in, nip, cl) : Raw8{0, 0};
       for (uint32_t j = lane; j < (uint32_t)len; j += 64) dst[j] = src[j];
       ip = nip;
       op += (uint32_t)len;
-      w = uni64(wn);
+      w = uni64(finish8(wn));
     } else {  // copy
       uint32_t hdr, len, off;
       const uint32_t kind = c & 3u;
@@ -221,7 +241,7 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
         fenced = op;
       }
       const uint32_t nip = ip + hdr;
-      const uint64_t wn = nip < cl ? load8<kLds>(in, nip, cl) : 0;
+      const Raw8 wn = nip < cl ? issue8<kLds>(in, nip, cl) : Raw8{0, 0};
       // byte j of the copy is out[op - off + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it.
       if (lane < len) {
@@ -230,7 +250,7 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
       }
       ip = nip;
       op += len;
-      w = uni64(wn);
+      w = uni64(finish8(wn));
     }
     // LDS variant: one wave's LDS accesses execute in issue order, so a copy
     // reads the bytes earlier tags wrote without waiting for the writes; the
