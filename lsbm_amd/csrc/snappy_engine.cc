@@ -19,6 +19,7 @@ hipError_t launch_snappy_length(const SnapLenArgs& a, int grid, hipStream_t stre
 hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream);
+hipError_t launch_snappy_compress_large(const SnapEncArgs& a, int grid, hipStream_t stream);
 
 namespace {
 
@@ -49,24 +50,19 @@ __attribute__((visibility("default"))) int lsbm_snappy_compress_dev(
   const int rc = engine_current_cus(&cus);
   if (rc != LSBM_OK) return rc;
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const int grid = wave_grid(cus, n, kSnapEncWgsPerCu);
-  // hash tables of fragments too large for LDS: one per workgroup, stream-ordered
-  void* scratch = nullptr;
-  const size_t scratch_bytes = (size_t)grid * kSnapMaxTable * sizeof(uint16_t);
-  hipError_t e = hipMallocAsync(&scratch, scratch_bytes, s);
-  if (e != hipSuccess) return engine_fail_hip(e, "hipMallocAsync(snappy scratch)");
   SnapEncArgs a = {};
   a.base = static_cast<const uint8_t*>(d_base);
   a.offsets = d_offsets;
   a.out = d_out;
   a.out_offsets = d_out_offsets;
   a.out_len = d_out_len;
-  a.scratch = static_cast<uint16_t*>(scratch);
   a.n = n;
-  e = launch_snappy_compress(a, grid, s);
-  const hipError_t ef = hipFreeAsync(scratch, s);
+  // pass 1: one-fragment blocks that fit a 22 KiB LDS slice; pass 2: the ones
+  // it deferred (out_len = kSnapDeferred), scanned 64 per wave
+  hipError_t e = launch_snappy_compress(a, wave_grid(cus, n, kSnapEncWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_compress_kernel");
-  return ef == hipSuccess ? LSBM_OK : engine_fail_hip(ef, "hipFreeAsync(snappy scratch)");
+  e = launch_snappy_compress_large(a, wave_grid(cus, (n + 63) / 64, kSnapEncLargeWgsPerCu), s);
+  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_compress_large_kernel");
 }
 
 __attribute__((visibility("default"))) int lsbm_snappy_uncompressed_length_dev(

@@ -583,21 +583,39 @@ remainder:
   return op;
 }
 
+// Per-wave setup shared by both encoder passes: lane k's offsets and skips of
+// probes k and 64 + k of a search from position 0 (skip 32), and the zeroed
+// hash-bucket counters at `buckets`.
+struct EncWave {
+  uint32_t off32, sk32, off64, sk64;
+  uint32_t* buckets;
+};
+
+__device__ __forceinline__ EncWave enc_wave(uint32_t* buckets, uint32_t lane) {
+  EncWave w;
+  probe_positions(0, 32, lane, &w.off32, &w.sk32);
+  const uint32_t p63 = __builtin_amdgcn_readlane(w.off32, 63), s63 = __builtin_amdgcn_readlane(w.sk32, 63);
+  probe_positions(p63 + (s63 >> 5), s63 + (s63 >> 5), lane, &w.off64, &w.sk64);
+  w.buckets = buckets;
+  for (uint32_t j = lane; j < kSnapEncBuckets / 4; j += 64) buckets[j] = 0;  // zero between searches
+  wave_order();
+  return w;
+}
+
+// varint32 preamble of block b; returns its size
+__device__ __forceinline__ uint32_t write_preamble(uint8_t* out, uint32_t n, uint32_t lane) {
+  uint32_t pre = 1;
+  while (pre < 5 && (n >> (7 * pre)) != 0) pre++;
+  if (lane < pre) out[lane] = (uint8_t)(((n >> (7 * lane)) & 127u) | (lane + 1 < pre ? 128u : 0u));
+  return pre;
+}
+
+// Pass 1: every block that is one fragment fitting the wave's 22 KiB slice
+// (fragment bytes and table in LDS, 7 waves per CU).  Larger blocks are
+// marked kSnapDeferred for pass 2.
 __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncArgs a) {
   const uint32_t lane = threadIdx.x;
-  uint16_t* const gtable = a.scratch + (uint64_t)blockIdx.x * kSnapMaxTable;
-  // probes k = lane and k = 64 + lane of a search from position 0, skip 32
-  uint32_t off32 = 0, sk32 = 0, off64 = 0, sk64 = 0;
-  probe_positions(0, 32, lane, &off32, &sk32);
-  {
-    const uint32_t p63 = __builtin_amdgcn_readlane(off32, 63), s63 = __builtin_amdgcn_readlane(sk32, 63);
-    probe_positions(p63 + (s63 >> 5), s63 + (s63 >> 5), lane, &off64, &sk64);
-  }
-  // hash-bucket counters of the batched search, behind the fragment's slice;
-  // zero between searches (every search clears what it counted)
-  uint32_t* const buckets = reinterpret_cast<uint32_t*>(smem + kSnapEncSlice);
-  for (uint32_t j = lane; j < kSnapEncBuckets / 4; j += 64) buckets[j] = 0;
-  wave_order();
+  const EncWave w = enc_wave(reinterpret_cast<uint32_t*>(smem + kSnapEncSlice), lane);
 #ifdef LSBM_SNAP_STAMPS
   Stamps sa = {};
   sa.t = __builtin_amdgcn_s_memtime();
@@ -610,34 +628,23 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
       continue;
     }
     const uint32_t n = (uint32_t)len;
-    uint8_t* const out = a.out + a.out_offsets[b];
-    // varint32 preamble
-    uint32_t pre = 1;
-    while (pre < 5 && (n >> (7 * pre)) != 0) pre++;
-    if (lane < pre) out[lane] = (uint8_t)(((n >> (7 * lane)) & 127u) | (lane + 1 < pre ? 128u : 0u));
-    uint64_t op = pre;
-    for (uint32_t pos = 0; pos < n; pos += kSnapFragment) {
-      const uint32_t fn = n - pos < kSnapFragment ? n - pos : kSnapFragment;
-      const uint32_t tsize = table_size_for(fn);
-      const uint8_t* g = a.base + s + pos;
-      if (2 * tsize + fn + 4 <= kSnapEncSlice) {  // + the staged copy's last dword
-        uint16_t* table = reinterpret_cast<uint16_t*>(smem);
-        uint8_t* lin = smem + 2 * tsize;
-        for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
-        stage_to_lds(lin, g, fn, lane);
-        wave_phase();
-        SNAP_STAMP(0);  // staging, table zeroing, preamble
-        op = compress_fragment<true>(lin, fn, table, tsize, out, op, lane, off32, sk32, off64, sk64, buckets SNAP_STAMPS_ARG);
-        wave_phase();
-      } else {
-        for (uint32_t j = lane; j < tsize; j += 64) gtable[j] = 0;
-        wave_phase();
-        SNAP_STAMP(0);
-        op = compress_fragment<false>(g, fn, gtable, tsize, out, op, lane, off32, sk32, off64, sk64, buckets SNAP_STAMPS_ARG);
-        wave_phase();
-      }
+    const uint32_t tsize = table_size_for(n);
+    if (n > kSnapFragment || 2 * tsize + n + 4 > kSnapEncSlice) {  // + the staged copy's last dword
+      if (lane == 0) a.out_len[b] = kSnapDeferred;
+      continue;
     }
-    if (lane == 0) a.out_len[b] = op;
+    uint8_t* const out = a.out + a.out_offsets[b];
+    const uint64_t op = write_preamble(out, n, lane);
+    uint16_t* table = reinterpret_cast<uint16_t*>(smem);
+    uint8_t* lin = smem + 2 * tsize;
+    for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
+    stage_to_lds(lin, a.base + s, n, lane);
+    wave_phase();
+    SNAP_STAMP(0);  // staging, table zeroing, preamble
+    const uint64_t end = compress_fragment<true>(lin, n, table, tsize, out, op, lane, w.off32, w.sk32, w.off64,
+                                                 w.sk64, w.buckets SNAP_STAMPS_ARG);
+    wave_phase();
+    if (lane == 0) a.out_len[b] = end;
   }
 #ifdef LSBM_SNAP_STAMPS
   if (lane == 0) {
@@ -645,6 +652,41 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
     atomicAdd(&g_snap_stamps[9], 1ull);
   }
 #endif
+}
+
+// Pass 2: the deferred blocks, found 64 at a time by ballot, fragment by
+// 64 KiB fragment: the hash table (up to 2^15 entries, 64 KiB) in LDS, the
+// fragment bytes read from global memory.  No global scratch.
+__global__ __launch_bounds__(kSnapThreads) void snappy_compress_large_kernel(SnapEncArgs a) {
+  const uint32_t lane = threadIdx.x;
+  const EncWave w = enc_wave(reinterpret_cast<uint32_t*>(smem + 2 * kSnapMaxTable), lane);
+  uint16_t* const table = reinterpret_cast<uint16_t*>(smem);
+#ifdef LSBM_SNAP_STAMPS
+  Stamps sa = {};
+  sa.t = __builtin_amdgcn_s_memtime();
+#endif
+  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+    const uint64_t i = c + lane;
+    uint64_t pend = __ballot(i < a.n && a.out_len[i] == kSnapDeferred);
+    while (pend) {
+      const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t s = a.offsets[b];
+      const uint32_t n = (uint32_t)(a.offsets[b + 1] - s);
+      uint8_t* const out = a.out + a.out_offsets[b];
+      uint64_t op = write_preamble(out, n, lane);
+      for (uint32_t pos = 0; pos < n; pos += kSnapFragment) {
+        const uint32_t fn = n - pos < kSnapFragment ? n - pos : kSnapFragment;
+        const uint32_t tsize = table_size_for(fn);
+        for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
+        wave_phase();
+        op = compress_fragment<false>(a.base + s + pos, fn, table, tsize, out, op, lane, w.off32, w.sk32, w.off64,
+                                      w.sk64, w.buckets SNAP_STAMPS_ARG);
+        wave_phase();
+      }
+      if (lane == 0) a.out_len[b] = op;
+    }
+  }
 }
 
 }  // namespace
@@ -668,6 +710,16 @@ hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStr
 
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(kSnapThreads), kSnapEncLds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_compress_large(const SnapEncArgs& a, int grid, hipStream_t stream) {
+  // 64.5 KiB of dynamic LDS: above the default dynamic limit, within gfx950's
+  // 160 KiB per workgroup
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&snappy_compress_large_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSnapEncLargeLds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(snappy_compress_large_kernel, dim3(grid), dim3(kSnapThreads), kSnapEncLargeLds, stream, a);
   return hipGetLastError();
 }
 

@@ -6,9 +6,10 @@
 namespace lsbm {
 
 // One wave per block, one wave per workgroup.  A block whose working set fits
-// the wave's LDS slice is decoded / encoded in LDS; a larger one runs the same
-// algorithm against global memory (output, and the encoder's hash table in a
-// per-workgroup scratch slice).
+// the wave's LDS slice is decoded / encoded in LDS in a first pass; a larger
+// one is left to a second pass with larger slices, or against global memory
+// (the decoder's output; the encoder's fragment bytes, its table staying in
+// LDS).
 constexpr uint32_t kSnapThreads = 64;
 // decoder slices hold the compressed bytes + 8 pad + the output window: pass 1
 // uses small slices (more waves in flight), pass 2 large ones
@@ -30,6 +31,11 @@ constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
 constexpr uint32_t kSnapDecWgsPerCu = 160 * 1024 / kSnapDecLds;  // LDS-limited residency
 constexpr uint32_t kSnapDecLargeWgsPerCu = 160 * 1024 / kSnapDecLdsLarge;
 constexpr uint32_t kSnapEncWgsPerCu = 160 * 1024 / kSnapEncLds;
+// encoder pass 2 (blocks that pass 1 cannot hold): the largest hash table in
+// LDS (2^15 entries), fragment bytes from global memory; 2 waves per CU
+constexpr uint32_t kSnapEncLargeLds = 2 * kSnapMaxTable + kSnapEncBuckets;
+constexpr uint32_t kSnapEncLargeWgsPerCu = 160 * 1024 / kSnapEncLargeLds;
+constexpr uint64_t kSnapDeferred = ~0ull - 1;  // out_len of a block left for pass 2
 
 struct SnapLenArgs {
   const uint8_t* base;
@@ -55,7 +61,6 @@ struct SnapEncArgs {
   uint8_t* out;
   const uint64_t* out_offsets;  // compressed i starts at out + out_offsets[i]
   uint64_t* out_len;            // compressed size (UINT64_MAX: block >= 2^32 bytes)
-  uint16_t* scratch;            // gridDim.x * kSnapMaxTable entries (large fragments)
   uint64_t n;
 };
 
