@@ -22,7 +22,7 @@ constexpr uint32_t kSnapEncSlice = 22528;
 constexpr uint32_t kSnapEncBuckets = 512;
 constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
 #ifndef LSBM_SNAP_PROBES
-#define LSBM_SNAP_PROBES 16
+#define LSBM_SNAP_PROBES 24
 #endif
 constexpr uint32_t kSnapProbes = LSBM_SNAP_PROBES;  // match-search probes per wave step (<= 64)
 constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (oracle/snappy_oracle.c)
