@@ -9,8 +9,11 @@ of every block, util/crc32c.cc:286-329).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-With N > 1 it is launched by torch.distributed.run, one process per GPU; each
-rank checksums its own shard of 10M x 4 KiB blocks (BASELINE.json configs[4]:
+With N > 1 it runs one process per GPU under torch.distributed.run: when
+WORLD_SIZE is unset, bench.py starts `python -m torch.distributed.run
+--nproc-per-node N ... bench.py` itself as a child process (before any GPU
+call) and exits with its return code; a WORLD_SIZE that differs from --gpus is
+an error.  Each rank checksums its own shard of 10M x 4 KiB blocks (BASELINE.json configs[4]:
 80M blocks over 8 GPUs; weak scaling, no data-path collective: blocks are
 independent).  --blocks overrides the per-GPU block count.  Timing: W untimed steps, barrier + synchronize, K
 steps between HIP events on the launch stream, barrier + synchronize, max over
@@ -52,7 +55,45 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="aggregate CPU-seconds for the cpu_baseline sample")
+    p.add_argument("--dump-samples", default="", help=argparse.SUPPRESS)  # tests: per-rank CRCs
     return p.parse_args()
+
+
+def usable_cores():
+    """Host cores this process may run on: the affinity mask, capped by a
+    cgroup CPU quota when one is set (the GPU box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    for path, conv in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                       ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), None])):
+        try:
+            with open(path) as f:
+                q = conv(f.read())
+        except OSError:
+            continue
+        try:
+            if q[0] != "max" and int(q[0]) > 0:
+                period = int(q[1]) if q[1] else int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                quota = max(1, int(q[0]) // period)
+        except (OSError, ValueError, IndexError):
+            pass
+        break
+    return (min(n, quota) if quota else n), n, quota
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without WORLD_SIZE: run this script under
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU)
+    and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def shard_range(n_total, rank, world):
@@ -99,10 +140,11 @@ def load_traffic(workload):
     return None
 
 
-def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
+def cpu_baseline(host, gpu_crcs, cpu_seconds):
     """Time the CPU CRC-32C on the host: the reference's own util/crc32c.cc
     (oracle/_ref, built from /root/reference) when present, else the oracle's
-    plain-C restatement of it.  Also cross-checks the GPU results on the sample."""
+    plain-C restatement of it.  `host` is a host copy of the whole device
+    batch; every block is also cross-checked against the GPU results."""
     import subprocess
     ref = os.path.join(REPO, "oracle", "_ref", "libref_crc32c.so")
     port = os.path.join(REPO, "oracle", "liboracle_crc32c.so")
@@ -117,26 +159,24 @@ def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                   ctypes.c_void_p, ctypes.c_int]
-    oracle = ctypes.CDLL(port if os.path.exists(port) else ref)
-    # host bytes of the first `sample_blocks` blocks of rank 0's buffer
-    from tests.golden.splitmix import stream_bytes
-    data = stream_bytes(SEED, 0, sample_blocks * BLOCK)
-    out = np.empty(sample_blocks, dtype=np.uint32)
-    threads = max(1, min(16, os.cpu_count() or 1))
-    f(data.ctypes.data, BLOCK, BLOCK, sample_blocks, out.ctypes.data, threads)  # warm
-    mismatches = int(np.count_nonzero(out != gpu_crcs[:sample_blocks]))
+    n = host.size // BLOCK
+    out = np.empty(n, dtype=np.uint32)
+    threads, affinity, quota = usable_cores()
+    threads = min(threads, 256)
+    f(host.ctypes.data, BLOCK, BLOCK, n, out.ctypes.data, threads)  # warm + cross-check
+    mismatches = int(np.count_nonzero(out != gpu_crcs[:n]))
     passes, t0 = 0, time.perf_counter()
-    while True:
-        f(data.ctypes.data, BLOCK, BLOCK, sample_blocks, out.ctypes.data, threads)
+    while True:  # >= 2 passes, >= 1 s wall, ~cpu_seconds of CPU work, <= 30 s
+        f(host.ctypes.data, BLOCK, BLOCK, n, out.ctypes.data, threads)
         passes += 1
         el = time.perf_counter() - t0
-        if el * threads >= cpu_seconds or el > 30:
+        if (passes >= 2 and el >= 1.0 and el * threads >= cpu_seconds) or el > 30:
             break
-    gib = passes * sample_blocks * BLOCK / 2**30
+    gib = passes * n * BLOCK / 2**30
     # one core, bounded to ~3 s (1 thread and all threads)
     p1, t1 = 0, time.perf_counter()
     while True:
-        f(data.ctypes.data, BLOCK, BLOCK, 8192, out.ctypes.data, 1)
+        f(host.ctypes.data, BLOCK, BLOCK, 8192, out.ctypes.data, 1)
         p1 += 1
         el1 = time.perf_counter() - t1
         if el1 >= 3.0:
@@ -149,11 +189,11 @@ def cpu_baseline(sample_blocks, gpu_crcs, cpu_seconds):
                 break
     except OSError:
         pass
-    del oracle
     return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{passes} passes x {sample_blocks} x {BLOCK} B blocks (first blocks of "
-                      f"the rank-0 buffer, host copy), crc32c::Value slice-by-4, "
-                      f"{threads} pthreads, {el:.1f} s wall; {cpu_model}",
+            "sample": f"{passes} passes x {n} x {BLOCK} B blocks (host copy of the whole "
+                      f"device batch), crc32c::Value slice-by-4, {threads} pthreads = all "
+                      f"usable cores (affinity {affinity}, cgroup quota {quota or 'none'}), "
+                      f"{el:.1f} s wall; {cpu_model}",
             "single_thread": {"value": round(p1 * 8192 * BLOCK / 2**30 / el1, 3), "unit": "GiB/s",
                               "cores": 1, "sample": f"{p1} passes x 8192 blocks, {el1:.1f} s"},
             "gpu_mismatches_on_sample": mismatches}
@@ -195,14 +235,17 @@ def host_staged(engine, data, gpu_crcs, n_blocks, reps=3):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        return 2
     # LSBM_BENCH_DEVICES lets a rehearsal put several ranks on fewer GPUs;
     # LSBM_BENCH_BACKEND=gloo rehearses the multi-rank flow without RCCL.
     ndev = int(os.environ.get("LSBM_BENCH_DEVICES", "0")) or torch.cuda.device_count()
@@ -262,11 +305,17 @@ def main():
     workload = f"{n} x {BLOCK} B device-resident blocks per GPU, batched crc32c::Value"
     traffic = load_traffic(workload)
 
+    if args.dump_samples:  # tests/test_multirank_gpu.py checks these against the oracle
+        idx = np.unique(np.concatenate([np.arange(min(n, 64)), np.arange(max(0, n - 64), n),
+                                        np.random.default_rng(rank).integers(0, n, 128)]))
+        np.savez(f"{args.dump_samples}.rank{rank}.npz", idx=idx, seed=SEED + rank, n=n,
+                 crc=out.cpu().numpy().view(np.uint32)[idx], world=world, t_max=t_max)
+
     cpu = staged = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gpu_crcs = out.cpu().numpy().view(np.uint32)
         staged = host_staged(engine, data, gpu_crcs, min(n, 1 << 18))
-        cpu = cpu_baseline(min(n, 65536), gpu_crcs, args.cpu_seconds)
+        cpu = cpu_baseline(data.cpu().numpy(), gpu_crcs, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -305,7 +354,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

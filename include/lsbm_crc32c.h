@@ -93,18 +93,24 @@ int lsbm_crc32c_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64
                            uint32_t* d_nbad, uint32_t flags, void* stream);
 
 /* ---- SSTable block trailers over a device-resident file image ----
- * d_handles holds n_blocks BlockHandles as {offset, size} uint64 pairs
- * (table/format.h:22-50).  The block occupies file[offset, offset+size) and its
- * 5-byte trailer [type u8][Mask(crc32c(block || type)) LE32] follows it. */
+ * d_file is file_bytes long; d_handles holds n_blocks BlockHandles as
+ * {offset, size} uint64 pairs (table/format.h:22-50).  The block occupies
+ * file[offset, offset+size) and its 5-byte trailer
+ * [type u8][Mask(crc32c(block || type)) LE32] follows it.  A handle whose
+ * size + 5 bytes do not fit inside file_bytes is ReadBlock's "truncated block
+ * read" (table/format.cc:88-91): no byte of it is read or written, it is
+ * counted into *d_nbad (when non-NULL) and, for verify, d_ok[i] = 0.  Callers
+ * that need to tell it from a checksum mismatch compare the handle with
+ * file_bytes (include/lsbm/table_checksum.h does). */
 /* WriteRawBlock (table/table_builder.cc:237-255): write each trailer, with
  * type = d_types[i] (CompressionType, include/leveldb/options.h:24-29). */
-int lsbm_sst_seal_dev(uint8_t* d_file, const uint64_t* d_handles, const uint8_t* d_types,
-                      uint64_t n_blocks, void* stream);
-/* ReadBlock verify (table/format.cc:95-103): d_ok[i] = 1 iff
- * Unmask(DecodeFixed32(trailer+1)) == Value(block || type); mismatches are
+int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
+                      const uint8_t* d_types, uint64_t n_blocks, uint32_t* d_nbad, void* stream);
+/* ReadBlock verify (table/format.cc:95-103): d_ok[i] = 1 iff the block fits and
+ * Unmask(DecodeFixed32(trailer+1)) == Value(block || type); failures are
  * added to *d_nbad when non-NULL. */
-int lsbm_sst_verify_dev(const uint8_t* d_file, const uint64_t* d_handles, uint64_t n_blocks,
-                        uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+int lsbm_sst_verify_dev(const uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
+                        uint64_t n_blocks, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
 
 /* ---- WAL / MANIFEST log records over a device-resident log image ----
  * common/log_format.h: 32 KiB log blocks of physical records, each a 7-byte

@@ -108,6 +108,15 @@ __device__ __forceinline__ uint32_t fin_lds(const uint32_t* lds, uint32_t v, uin
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
+// XOR of v over the 8 lanes of a group (DPP: swap neighbours, swap pairs,
+// then mirror the two quads of each half-row); every lane gets the result.
+__device__ __forceinline__ uint32_t group_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return v;
+}
+
 // Copy the prebuilt LDS image (DevConsts::lds_image) into LDS: every thread
 // issues all of its 16-B loads before its first LDS write (one round trip).
 __device__ __forceinline__ void load_lds_tables(uint32_t* lds, const DevConsts* __restrict__ dc) {
@@ -141,10 +150,7 @@ __device__ __forceinline__ uint32_t merge_braids(const uint32_t* lds, uint32_t c
   u = adv4_lds(lds, u) ^ c3;
   // to the end of the row: A^(128 - (16li + 16)) then A^4 = A^(116 - 16li)
   u = fin_lds(lds, u, lane_fin);
-  u ^= __shfl_xor(u, 1, kGroupLanes);
-  u ^= __shfl_xor(u, 2, kGroupLanes);
-  u ^= __shfl_xor(u, 4, kGroupLanes);
-  return u;
+  return group_xor(u);
 }
 
 }  // namespace lsbm

@@ -87,6 +87,19 @@ void build_consts(DevConsts* c) {
     memcpy(&c->lds_image[kNibRowPow / 4 + i * 128], c->pow_nib[7 + i], 512);
   memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
   memset(c->zero16, 0, sizeof(c->zero16));
+  // column forms for the units kernel: A^(128 k) and A^e, e = -127 .. 1
+  {
+    const gf2::Mat row = gf2::byte_pow(kRowBytes);
+    gf2::Mat m = gf2::identity();
+    for (uint32_t k = 0; k < kShiftCols; k++) {
+      memcpy(c->shift_cols[k], m.col, sizeof(m.col));
+      m = gf2::mul(row, m);
+    }
+    for (uint32_t i = 0; i < kFinCols; i++) {
+      const gf2::Mat f = gf2::byte_pow((int64_t)i - 127);
+      memcpy(c->fin_cols[i], f.col, sizeof(f.col));
+    }
+  }
 }
 
 void init_device(int dev, DeviceState* st) {
@@ -150,21 +163,22 @@ int grid_for(const DeviceState* st, uint64_t n_blocks) {
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(wgs, (uint64_t)st->num_cus));
 }
 
+// A^-4(~0): the virtual init bytes of crc32c::Value (init 0), see crc32c_kernels.hip
+uint32_t u_noinit() {
+  static const uint32_t u = gf2::apply(gf2::byte_pow(-4), 0xffffffffu);
+  return u;
+}
+
+// One launch, no allocation, no host sync: graph-capturable like the fixed path.
 int run_ragged(RaggedArgs a, hipStream_t stream) {
   DeviceState* st = nullptr;
   int rc = current_device(&st);
   if (rc != LSBM_OK) return rc;
   if (a.n == 0) return LSBM_OK;
   a.dc = st->d_consts;
-  if (a.dbg_hi == 0) a.dbg_hi = ~0ull;  // debug-bounds builds: unknown range = unchecked
-  // per-block accumulators, stream-ordered so the call stays asynchronous
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&a.acc), a.n * sizeof(uint32_t), stream);
-  if (e != hipSuccess) return fail_hip(e, "hipMallocAsync(acc)");
-  e = hipMemsetAsync(a.acc, 0, a.n * sizeof(uint32_t), stream);
-  if (e == hipSuccess) e = launch_ragged(a, (int)st->num_cus, stream);
-  hipError_t e2 = hipFreeAsync(a.acc, stream);
-  if (e != hipSuccess) return fail_hip(e, "crc32c_units_kernel");
-  return e2 == hipSuccess ? LSBM_OK : fail_hip(e2, "hipFreeAsync(acc)");
+  a.u_noinit = u_noinit();
+  const hipError_t e = launch_ragged(a, (int)st->num_cus, stream);
+  return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_units_kernel");
 }
 
 // ---- host-staged pipeline ----
@@ -177,7 +191,6 @@ struct Slot {
   uint64_t* d_off = nullptr;
   uint32_t* d_init = nullptr;
   uint32_t* d_out = nullptr;
-  uint32_t* d_acc = nullptr;
   uint64_t cap_bytes = 0, cap_blocks = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
@@ -202,10 +215,8 @@ void free_slot_buffers(Slot& s) {
   if (s.d_off) hipFree(s.d_off);
   if (s.d_init) hipFree(s.d_init);
   if (s.d_out) hipFree(s.d_out);
-  if (s.d_acc) hipFree(s.d_acc);
   s.h_data = nullptr; s.h_off = nullptr; s.h_init = nullptr; s.h_out = nullptr;
   s.d_data = nullptr; s.d_off = nullptr; s.d_init = nullptr; s.d_out = nullptr;
-  s.d_acc = nullptr;
   s.cap_bytes = s.cap_blocks = 0;
 }
 
@@ -232,7 +243,6 @@ hipError_t reserve_slot(Slot& s, uint64_t bytes, uint64_t blocks) {
   if ((e = hipMalloc(&s.d_off, (blocks + 1) * 8)) != hipSuccess) return e;
   if ((e = hipMalloc(&s.d_init, blocks * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&s.d_out, blocks * 4)) != hipSuccess) return e;
-  if ((e = hipMalloc(&s.d_acc, blocks * 4)) != hipSuccess) return e;
   s.cap_bytes = bytes;
   s.cap_blocks = blocks;
   return hipSuccess;
@@ -336,8 +346,6 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
   a.len = len;
   a.extents = kExtFixed;
   a.n = n_blocks;
-  a.dbg_lo = reinterpret_cast<uint64_t>(d_base);
-  a.dbg_hi = a.dbg_lo + (n_blocks - 1) * stride + len;
   a.init = d_init;
   a.out = d_out;
   a.flags = flags;
@@ -399,10 +407,11 @@ __attribute__((visibility("default"))) int lsbm_crc32c_verify_dev(
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
-__attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file,
+__attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes,
                                                              const uint64_t* d_handles,
                                                              const uint8_t* d_types,
-                                                             uint64_t n_blocks, void* stream) {
+                                                             uint64_t n_blocks, uint32_t* d_nbad,
+                                                             void* stream) {
   if (n_blocks == 0) return LSBM_OK;
   if (!d_file || !d_handles || !d_types) return fail(LSBM_ERR_INVALID, "null pointer");
   RaggedArgs a = {};
@@ -412,11 +421,14 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file,
   a.extents = kExtHandles;
   a.types = d_types;
   a.n = n_blocks;
+  a.nbad = d_nbad;
+  a.limit = file_bytes;
   a.mode = kModeSstSeal;
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
 __attribute__((visibility("default"))) int lsbm_sst_verify_dev(const uint8_t* d_file,
+                                                               uint64_t file_bytes,
                                                                const uint64_t* d_handles,
                                                                uint64_t n_blocks, uint8_t* d_ok,
                                                                uint32_t* d_nbad, void* stream) {
@@ -426,6 +438,7 @@ __attribute__((visibility("default"))) int lsbm_sst_verify_dev(const uint8_t* d_
   a.base = d_file;
   a.handles = d_handles;
   a.extents = kExtHandles;
+  a.limit = file_bytes;
   a.n = n_blocks;
   a.ok = d_ok;
   a.nbad = d_nbad;
@@ -450,8 +463,6 @@ __attribute__((visibility("default"))) int lsbm_log_seal_dev(uint8_t* d_log, uin
   a.out = d_masked;
   a.nbad = d_nbad;
   a.mode = kModeLogSeal;
-  a.dbg_lo = reinterpret_cast<uint64_t>(d_log);
-  a.dbg_hi = a.dbg_lo + log_bytes;
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
@@ -471,8 +482,6 @@ __attribute__((visibility("default"))) int lsbm_log_verify_dev(const uint8_t* d_
   a.ok = d_ok;
   a.nbad = d_nbad;
   a.mode = kModeLogVerify;
-  a.dbg_lo = reinterpret_cast<uint64_t>(d_log);
-  a.dbg_hi = a.dbg_lo + log_bytes;
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
@@ -598,11 +607,8 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
     a.flags = flags;
     a.mode = kModeOut;
     a.dc = st->d_consts;
-    a.acc = s.d_acc;
-    a.dbg_lo = reinterpret_cast<uint64_t>(s.d_data);
-    a.dbg_hi = a.dbg_lo + pos;
-    e = hipMemsetAsync(s.d_acc, 0, cnt * 4, s.stream);
-    if (e == hipSuccess) e = launch_ragged(a, (int)st->num_cus, s.stream);
+    a.u_noinit = u_noinit();
+    e = launch_ragged(a, (int)st->num_cus, s.stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);

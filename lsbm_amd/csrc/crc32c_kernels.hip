@@ -3,8 +3,9 @@
 // crc32c_fixed_kernel   fixed-stride, len % 128 == 0, 16-B aligned blocks
 //                       (SSTable-sized 4 KiB and 64 KiB batches; the headline)
 // crc32c_units_kernel   any extents, any alignment (offsets[] batches, verify,
-// crc32c_finish_kernel  SSTable trailer seal / verify): 32-row units per lane
-//                       group, partial CRCs xor-ed per block, then finished
+//                       SSTable trailer seal / verify, log headers): <= 48-row
+//                       units per lane group, summed per block inside the wave
+//                       and finished in registers
 // fill_splitmix64_kernel, stream_read_kernel   benchmark helpers
 //
 // Both CRC kernels compute, per block, exactly what lsbm's
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 #endif
 }
 // ---------------------------------------------------------------------------
-// Ragged path: units kernel + finish kernel.
+// Ragged path: one kernel, every output mode.
 //
 // Frame.  Rows are 128-B aligned in the absolute address space, so every load
 // is an aligned 16-B load whatever the block's alignment.  For block [s, e):
@@ -192,12 +193,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 //   * the init register v = init ^ ~0 is injected as 4 virtual bytes
 //     u = A^-4(v) at [s-4, s) (absorbing u from zero gives exactly v);
 //   * the frame ends z = frame_end - e bytes late: undone with A^-z.
-// Units.  The frame is cut into units of <= 32 rows (crc32c_types.h).  Each
-// wave walks a contiguous range of blocks and hands the next 8 units of the
-// range to its 8 lane groups, so most steps are uniform 32-row loops whatever
-// the block lengths.  A unit's raw CRC, shifted to the frame end by
-// A^(4096 k), is xor-ed into acc[block]; the finish kernel turns acc into
-// the CRC and applies the output mode.
+// Units.  The frame is cut into units of <= kMaxRows rows (crc32c_types.h).
+// Each wave walks a contiguous range of blocks and hands the next 8 units of
+// the range to its 8 lane groups.  A unit's raw CRC, shifted to the frame end
+// by A^(128 k), is summed with the other units of its block INSIDE the wave:
+// the units of a round are consecutive, so a segmented xor-scan over the 8
+// groups sums each block's units of the round, and the one block that is still
+// open at the end of a round carries its partial sum into the next round.  The
+// group holding a block's last unit finishes it in registers (A^-z, the mode:
+// CRC, verify, SSTable trailer, log header), so there is no accumulator array,
+// no atomics on the data path and no second kernel.
 // ---------------------------------------------------------------------------
 // Byte n of a little-endian word and below: (1 << 8n) - 1, n in [0, 4].
 __device__ __forceinline__ uint32_t low_bytes(int32_t n) {
@@ -229,6 +234,7 @@ typedef const __attribute__((address_space(1))) uint8_t* gptr_u8;
 
 constexpr uint64_t kLogHeaderSize = 7;  // common/log_format.h:30 (crc 4, length 2, type 1)
 constexpr uint64_t kLogNoHeader = ~0ull;  // ExtRaw.y of a header that is not inside the image
+constexpr uint64_t kTrailer = 5;        // table/format.h:84 kBlockTrailerSize
 
 __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) {
   ExtRaw r = {0, 0};
@@ -256,31 +262,38 @@ __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) 
   return r;
 }
 
-// A log record's header and payload lie inside the image [0, limit).
-__device__ __forceinline__ bool log_record_fits(const RaggedArgs& a, ExtRaw r) {
-  return r.y != kLogNoHeader && a.limit - r.x - kLogHeaderSize >= r.y;
-}
-
-// Block b's extent [s, e) as absolute addresses.
+// Block b's extent [s, e) as absolute addresses, whether the record fits the
+// image (log headers; SSTable handles whose n + 5 bytes must lie inside
+// `limit`, table/format.cc:88-91), and the address of its stored / written
+// checksum: the trailer's type byte (seal: e), the trailer's crc (verify: e,
+// the extent covers the type byte), the log header (log modes).  A record
+// that does not fit is empty here (no byte of it is read) and bad at finish.
 __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b, ExtRaw r,
-                                                uint64_t& s, uint64_t& e) {
+                                                uint64_t& s, uint64_t& e, bool& fits,
+                                                uint64_t& at) {
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
+  fits = true;
   if (a.extents == kExtLogHeaders) {
-    // CRC over [type || payload] = [h + 6, h + 7 + length) (common/log_reader.cc:231);
-    // a record that does not fit the image is empty here and bad in the finish kernel
-    const bool fits = log_record_fits(a, r);
+    // CRC over [type || payload] = [h + 6, h + 7 + length) (common/log_reader.cc:231)
+    fits = r.y != kLogNoHeader && a.limit - r.x - kLogHeaderSize >= r.y;
     s = base + (fits ? r.x + 6 : 0);
     e = fits ? s + 1 + r.y : s;
+    at = base + r.x;
   } else if (a.extents == kExtHandles) {
-    s = base + r.x;
-    e = s + r.y + (a.mode == kModeSstVerify ? 1u : 0u);  // verify covers the type byte
+    if (a.mode == kModeSstSeal || a.mode == kModeSstVerify)
+      fits = r.x <= a.limit && a.limit - r.x >= kTrailer && a.limit - r.x - kTrailer >= r.y;
+    s = base + (fits ? r.x : 0);
+    e = fits ? s + r.y + (a.mode == kModeSstVerify ? 1u : 0u) : s;  // verify covers the type
+    at = e;
   } else if (a.extents == kExtFixed) {
     s = base + b * a.stride;
     e = s + a.len;
+    at = e;
   } else {
     s = base + r.x;
     e = base + r.y;
     if (e < s) e = s;
+    at = e;
   }
 }
 
@@ -290,7 +303,7 @@ struct Frame {
   uint32_t q, rem;            // balanced split: units of q rows, the first rem of them q + 1
 };
 
-__device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e, uint32_t max_rows = kUnitRows) {
+__device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e, uint32_t max_rows) {
   Frame f;
   f.s = s;
   f.e = e;
@@ -324,18 +337,48 @@ __device__ __forceinline__ uint32_t shift_rows(const uint32_t* lds, const DevCon
   return v;
 }
 
+// M(v) for a matrix in column form spread over an 8-lane group: lane li holds
+// columns 4li .. 4li+3 (M(1 << b) for the bits b of v in [4li, 4li + 4)).
+// Every lane of the group receives M(v); every lane must execute it.
+__device__ __forceinline__ uint32_t cols_apply(u32x4 c, uint32_t v, uint32_t li) {
+  const uint32_t nib = v >> (4u * li);
+  const uint32_t r = xor3(c.x & (0u - (nib & 1u)), c.y & (0u - ((nib >> 1) & 1u)),
+                          c.z & (0u - ((nib >> 2) & 1u))) ^
+                     (c.w & (0u - ((nib >> 3) & 1u)));
+  return group_xor(r);
+}
+
+// A(t) for one byte t: the CRC register contribution of extending by a byte
+// (util/crc32c.cc:291-294 with l = 0), computed bitwise.
+__device__ __forceinline__ uint32_t advance_byte(uint32_t t) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) t = (t >> 1) ^ (0x82F63B78u & (0u - (t & 1u)));
+  return t;
+}
+
+// 4 bytes at an arbitrary address from the two aligned dwords covering them.
+__device__ __forceinline__ uint32_t unaligned_word(uint32_t lo, uint32_t hi, uint64_t addr) {
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)addr & 3u);
+}
+
 // Units kernel.  Each wave owns a contiguous range of blocks and walks it in
 // rounds of 8 units (one per lane group).  The loop is software-pipelined so
 // that no global-memory latency is exposed between rounds:
 //   * the extents of the next round's blocks are loaded one round ahead;
-//   * a round issues its first bank of row loads, THEN merges the previous
-//     round's braids (LDS work overlapping the loads), then streams its rows.
+//   * a round loads what its units' finish will need (shift and A^-z
+//     matrices, expected values, stored trailers) before its row loads, and
+//     consumes them one round later, so no wait ever drains the row loads;
+//   * a round issues its first bank of row loads, THEN retires the previous
+//     round (merge, shift, in-wave sum, finish: LDS and ALU work overlapping
+//     the loads), then streams its rows.
 //
 // kMaxRows is the longest unit: kUnitRows for general batches; kSstUnitRows for
 // SSTable trailers, whose blocks (4,117-4,123 B with the type byte, 33-34 rows)
 // then go through as ONE unit each, 8 blocks per round, no split and no shift.
-template <uint32_t kMaxRows>
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
+  args.mode = kMode;   // compile-time: lets the compiler drop the other modes' code
+  args.extents = kExt;
   const DevConsts* __restrict__ dc = args.dc;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
@@ -349,13 +392,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   const uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const uint32_t* __restrict__ init = args.init;
+  constexpr uint32_t mode = kMode;
   const uint32_t jl = lane < 8u ? lane : 8u;  // lanes 0..8 hold the walk's 9 blocks
-#ifdef LSBM_DEBUG_BOUNDS
-  if (threadIdx.x == 0 && blockIdx.x == 0)
-    printf("units: n %lu base %lx dbg [%lx, %lx) acc %p dc %p dummy %lx grid %u\n", (unsigned long)args.n,
-           (unsigned long)args.base, (unsigned long)args.dbg_lo, (unsigned long)args.dbg_hi, args.acc, dc,
-           (unsigned long)dummy, gridDim.x);
-#endif
   // extents (+ init) of blocks nb + jl, clamped into the range so that the
   // loads are unconditional; only lanes with nb + lane < b_hi use them
   auto prefetch = [&](uint64_t nb, ExtRaw& r, uint32_t& iv) {
@@ -373,24 +411,85 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   if (b_lo < b_hi) prefetch(cur_b, rj, ivj);
   load_lds_tables(g_lds, dc);  // overlaps the first extents' latency
 
-  // the previous round's braids and destination
+  // The block still open at the end of the last retired round and the xor of
+  // its units so far (wave-uniform); ~0 = none.
+  uint64_t carry_b = ~0ull;
+  uint32_t carry_v = 0;
+  // the previous round: braids, unit and block, and what its finish needs
   uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-  uint64_t pk = 0;
-  uint64_t pb = 0;
-  bool pact = false;
-  auto retire = [&]() {  // merge the previous round's braids into acc
-#if defined(LSBM_ABL_U_NOMERGE)  // diagnostic builds only (wrong CRCs)
-    const uint32_t raw = p0;
-#else
+  u32x4 pshift = {0, 0, 0, 0}, pfin = {0, 0, 0, 0};
+  uint32_t paux0 = 0, paux1 = 0;
+  uint64_t pk = 0, pb = 0, pat = 0;
+  bool pact = false, plast = false, pfits = true;
+
+  auto retire = [&]() {
     const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
-#endif
-    if (pact) {
-      const uint32_t contrib = shift_rows(g_lds, dc, raw, pk);
-#ifdef LSBM_DEBUG_BOUNDS
-      if (li == 0 && pb >= args.n) printf("ACC OOB wave %lu b %lu n %lu\n", (unsigned long)wave, (unsigned long)pb, (unsigned long)args.n);
-      else
-#endif
-      if (li == 0) atomicXor(args.acc + pb, contrib);
+    uint32_t v = cols_apply(pshift, raw, li);        // A^(128 (k mod 512))
+    if (pk >= kShiftCols) v = shift_rows(g_lds, dc, v, pk & ~(uint64_t)(kShiftCols - 1));
+    v = pact ? v : 0u;
+    const uint64_t key = pact ? pb : ~0ull;
+    // segmented inclusive xor-scan over the 8 groups (blocks non-decreasing in g)
+#pragma unroll
+    for (uint32_t d = 8; d < 64; d <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)v, d);
+      const uint64_t tk = (uint64_t)__shfl_up((unsigned long long)key, d);
+      if (lane >= d && tk == key) v ^= t;
+    }
+    if (pact && key == carry_b) v ^= carry_v;
+    // the block open after group 7 carries into the next round
+    const uint64_t key7 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), 56) << 32) |
+                          __builtin_amdgcn_readlane((uint32_t)key, 56);
+    const uint32_t last7 = __builtin_amdgcn_readlane((uint32_t)plast, 56);
+    carry_v = __builtin_amdgcn_readlane(v, 56);
+    carry_b = (key7 != ~0ull && !last7) ? key7 : ~0ull;
+    // finish: register after the block = A^-z(v) (A^(1-z) for the seal's type byte)
+    uint32_t l = cols_apply(pfin, v, li);
+    if (!(pact && plast)) return;
+    if constexpr (mode == kModeSstSeal) {  // table/table_builder.cc:245-249
+      if (!pfits) {
+        if (li == 0 && args.nbad) atomicAdd(args.nbad, 1u);
+        return;
+      }
+      const uint32_t typ = paux0 & 0xffu;
+      const uint32_t m = mask_crc((l ^ advance_byte(typ)) ^ 0xffffffffu);  // Extend(crc, &type, 1)
+      if (li < kTrailer)  // [type][masked crc LE32], one byte per lane
+        reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(li == 0 ? typ : m >> (8 * (li - 1)));
+      return;
+    }
+    if (li != 0) return;
+    const uint32_t crc = l ^ 0xffffffffu;
+    switch (mode) {
+      case kModeOut:
+        args.out[pb] = (args.flags & 1u) ? mask_crc(crc) : crc;
+        break;
+      case kModeVerify: {
+        const uint32_t got = (args.flags & 1u) ? mask_crc(crc) : crc;
+        const bool good = got == paux0;
+        args.ok[pb] = good ? 1 : 0;
+        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
+        break;
+      }
+      case kModeLogSeal: {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
+        if (!pfits) {
+          if (args.out) args.out[pb] = 0;
+          if (args.nbad) atomicAdd(args.nbad, 1u);
+          break;
+        }
+        uint8_t* h = reinterpret_cast<uint8_t*>(pat);
+        const uint32_t m = mask_crc(crc);
+        h[0] = (uint8_t)m;
+        h[1] = (uint8_t)(m >> 8);
+        h[2] = (uint8_t)(m >> 16);
+        h[3] = (uint8_t)(m >> 24);
+        if (args.out) args.out[pb] = m;
+        break;
+      }
+      default: {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+        const bool good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
+        args.ok[pb] = good ? 1 : 0;
+        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
+        break;
+      }
     }
   };
 
@@ -399,8 +498,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     // (8 units never span more than 9 blocks), an inclusive prefix sum over
     // the lanes' unit counts, then one ballot per group.  ALU + shuffles only:
     // the extents arrived during the previous round.
-    uint64_t sj = 0, ej = 0;
-    extent_from_raw(args, cur_b + lane, rj, sj, ej);
+    uint64_t sj = 0, ej = 0, atj = 0;
+    bool fj = true;
+    extent_from_raw(args, cur_b + lane, rj, sj, ej, fj, atj);
     const Frame ft = frame_of(sj, ej, kMaxRows);
     const bool vj = lane < 9u && cur_b + lane < b_hi;
     const uint32_t units_j = vj ? ft.units : 0u;
@@ -435,6 +535,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     f.q = (uint32_t)__shfl((int)ft.q, (int)jg);
     f.rem = (uint32_t)__shfl((int)ft.rem, (int)jg);
     const uint32_t iv = (uint32_t)__shfl((int)ivj, (int)jg);
+    const bool fits = __shfl((int)fj, (int)jg) != 0;
+    const uint64_t at = __shfl((unsigned long long)atj, (int)jg);
     const uint32_t o = my_t - pre_before;
     // the cursor after these 8 units, and the next round's extents
     const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
@@ -479,21 +581,39 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
         const int64_t t_s = (int64_t)f.s - 1 - (int64_t)row_a;
         if (t_s >= 0 && (t_s & 127) < 19 && (t_s >> 7) < (int64_t)rows) {
           rfs = (uint32_t)(t_s >> 7);
-#ifdef LSBM_DEBUG_BOUNDS
-          if (rfs > 1) printf("RFS %u b %lu o %u\n", rfs, (unsigned long)b, o);
-#endif
           ds = (int32_t)(t_s & 127) + 1;
           const int64_t ee = (int64_t)f.e - (int64_t)(row_a + (uint64_t)rfs * kRowBytes);
           de_s = ee < 64 ? (int32_t)ee : 64;
         }
+        // (only for a non-empty block: the chunk of byte e - 1 must overlap [s, e),
+        // or an empty block at the start of an allocation would read before it)
         const int64_t t_e = (int64_t)f.e - 1 - (int64_t)row_a;
-        if (t_e >= 0 && (t_e & 127) < 15 && (t_e >> 7) < (int64_t)rows &&
+        if (f.s < f.e && t_e >= 0 && (t_e & 127) < 15 && (t_e >> 7) < (int64_t)rows &&
             (uint32_t)(t_e >> 7) != rfs) {
           rfe = (uint32_t)(t_e >> 7);
           de_e = (int32_t)(t_e & 127) + 1;
+          // that chunk is read ONCE, by the early load below, never by the row
+          // loop: its bytes >= e may be another block's trailer or log header,
+          // which a seal in another wave can be writing right now, so two
+          // reads of it need not agree
+          r_hi = rfe;
         }
       }
     }
+    // What this round's finish needs is loaded after its rows and used one
+    // round later, behind the next round's first row loads (every load
+    // unconditional, from a valid address): the columns of A^(128 (k mod 512))
+    // and of A^-z / A^(1-z); expect[b] (verify), types[b] (seal), or the two
+    // aligned dwords holding a stored trailer / log header crc (verifies).
+    // Until then only these compact words stay live across the row loop.
+    const bool last = active && o + 1 == f.units;
+    const uint32_t zf = (uint32_t)((f.row0 + f.rows) * kRowBytes - f.e);  // < 128
+    const uint32_t fin_i = active ? (mode == kModeSstSeal ? 128u : 127u) - zf : 127u;
+    const uint32_t st_i = (active ? (uint32_t)(k & (kShiftCols - 1)) : 0u) | (fin_i << 16) |
+                          (last ? 1u << 24 : 0u) | (fits ? 1u << 25 : 0u) | (active ? 1u << 26 : 0u);
+    const uint32_t b_rel = (uint32_t)(b - b_lo);  // a wave's range is < 2^32 blocks
+    const uint32_t k_hi = (uint32_t)(k >> 9);     // shift beyond the columns (blocks > 64 KiB)
+
     // uniform trip count: the longest unit of the 8 groups
     uint32_t rows_max = rows;
     rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 8));
@@ -509,14 +629,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     auto row_addr = [&](uint32_t r) -> gptr_u32x4 {
       const bool ok = (r >= r_lo) & (r < r_hi);
       uint64_t p = ok ? row_a + (uint64_t)r * kRowBytes : dummy;
-#ifdef LSBM_DEBUG_BOUNDS  // diagnostic builds only: report and neutralise wild loads
-      if (p != dummy && (p + 16 <= args.dbg_lo || p >= args.dbg_hi)) {
-        printf("OOB wave %lu lane %u b %lu o %u r %u rows %u s %lx e %lx row_a %lx p %lx\n",
-               (unsigned long)wave, lane, (unsigned long)b, o, r, rows, (unsigned long)f.s,
-               (unsigned long)f.e, (unsigned long)row_a, (unsigned long)p);
-        p = dummy;
-      }
-#endif
       asm volatile("" : "+v"(p));
       return reinterpret_cast<gptr_u32x4>(p);
     };
@@ -525,14 +637,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     u32x4 ba[4], bb[4];
 #pragma unroll
     for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(k2));
-    // the chunk straddling e sits in the unit's last row (rfe = rows - 1): its
-    // bytes >= e are removed after the loop (below), from this early copy
+    // the chunk straddling e sits in the unit's last row (rfe = rows - 1): the
+    // row loop absorbs zeros for it, and its bytes < e are added after the
+    // loop (below) from this one copy
     uint64_t pe = rfe != ~0u ? row_a + (uint64_t)rfe * kRowBytes : dummy;
     asm volatile("" : "+v"(pe));
     const u32x4 wl = *reinterpret_cast<gptr_u32x4>(pe);
 
-    // while those loads fly: the init bytes and the previous round's merge
-    const uint32_t u = nib_lds_at(g_lds, kNibNeg4, iv ^ 0xffffffffu);  // A^-4(init ^ ~0)
+    // while those loads fly: the init bytes and the previous round's retire
+    const uint32_t u = (kExt != kExtLogHeaders && init) ? nib_lds_at(g_lds, kNibNeg4, iv ^ 0xffffffffu)  // A^-4(init ^ ~0)
+                            : args.u_noinit;
     retire();
 
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -547,14 +661,12 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     // and 1 of a unit: chunk c of row 0 has c <= s - 4 and the fix chunk has
     // c >= s - 19.
     auto absorb_start = [&](u32x4 w, uint32_t r) {
-#ifndef LSBM_ABL_U_NOFIX  // diagnostic builds only: skip the edge masking (wrong CRCs)
       if (rfs == r) {
         w.x = fix_word(w.x, ds, de_s, u, 0);
         w.y = fix_word(w.y, ds, de_s, u, 4);
         w.z = fix_word(w.z, ds, de_s, u, 8);
         w.w = fix_word(w.w, ds, de_s, u, 12);
       }
-#endif
       absorb(w, r);
     };
     // Every bank load is unconditional (rows past the unit read the pad): with
@@ -567,13 +679,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     absorb(ba[2], 2);
     absorb(ba[3], 3);
     // End fix.  The register kept per braid is the pre-lookup word c = s ^ w
-    // of the last row absorbed, so dropping the bytes >= e of that row is a
-    // plain xor after the loop: c ^= w & ~keep (lanes without rfe: de_e = 64,
-    // keep = ~0).  Computed here, pinned, so that no wait follows the loop.
-    uint32_t dx = wl.x & ~low_bytes(min(max(de_e, 0), 4));
-    uint32_t dy = wl.y & ~low_bytes(min(max(de_e - 4, 0), 4));
-    uint32_t dz = wl.z & ~low_bytes(min(max(de_e - 8, 0), 4));
-    uint32_t dw = wl.w & ~low_bytes(min(max(de_e - 12, 0), 4));
+    // of the last row absorbed, and the row loop absorbed w = 0 for the chunk
+    // straddling e, so adding its bytes < e is a plain xor after the loop:
+    // c ^= w & keep (lanes without rfe loaded the zero pad: 0).  Computed
+    // here, pinned, so that no wait follows the loop.
+    uint32_t dx = wl.x & low_bytes(min(max(de_e, 0), 4));
+    uint32_t dy = wl.y & low_bytes(min(max(de_e - 4, 0), 4));
+    uint32_t dz = wl.z & low_bytes(min(max(de_e - 8, 0), 4));
+    uint32_t dw = wl.w & low_bytes(min(max(de_e - 12, 0), 4));
     asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(dw));
     // fully unrolled (rows_max <= kMaxRows): a rolled loop got a vmcnt(0) at
     // its header, draining the bank in flight every 8 rows
@@ -590,115 +703,53 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
 #pragma unroll
       for (uint32_t k2 = 0; k2 < 4; k2++) absorb(ba[k2], r + 4 + k2);
     }
-#ifndef LSBM_ABL_U_NOFIX
     c0 ^= dx;
     c1 ^= dy;
     c2 ^= dz;
     c3 ^= dw;
-#endif
     // this round becomes the previous one
-#if defined(LSBM_ABL_U_NOMERGE)  // diagnostic builds only (wrong CRCs)
-    p0 = c0 ^ c1 ^ c2 ^ c3;
-    p1 = p2 = p3 = 0;
-#else
     p0 = c0;
     p1 = c1;
     p2 = c2;
     p3 = c3;
-#endif
-#if defined(LSBM_ABL_U_NOSHIFT) || defined(LSBM_ABL_U_NOMERGE)
-    pk = 0;
-#else
-    pk = k;
-#endif
-    pb = b;
-    pact = active;
+    pact = (st_i >> 26) & 1u;
+    plast = (st_i >> 24) & 1u;
+    pfits = (st_i >> 25) & 1u;
+    pb = b_lo + b_rel;
+    pk = ((uint64_t)k_hi << 9) | (st_i & 0x1ffu);
+    pat = at;
+    {
+      const uint32_t ks = st_i & 0xffffu, fi = (st_i >> 16) & 0xffu;
+      pshift = *reinterpret_cast<gptr_u32x4>(reinterpret_cast<uint64_t>(&dc->shift_cols[ks][4 * li]));
+      pfin = *reinterpret_cast<gptr_u32x4>(reinterpret_cast<uint64_t>(&dc->fin_cols[fi][4 * li]));
+      const bool need = plast && pfits;
+      uint64_t q0 = dummy, q1 = dummy;
+      if constexpr (mode == kModeVerify) {
+        q0 = need ? reinterpret_cast<uint64_t>(args.expect + pb) : dummy;
+      } else if constexpr (mode == kModeSstSeal) {
+        q0 = need ? reinterpret_cast<uint64_t>(args.types + pb) : dummy;
+      } else if constexpr (mode == kModeSstVerify || mode == kModeLogVerify) {
+        // the dwords holding bytes pat and pat + 3 (one dword when aligned:
+        // never a byte past the stored crc)
+        q0 = need ? (pat & ~3ull) : dummy;
+        q1 = need ? ((pat + 3) & ~3ull) : dummy;
+      }
+      asm volatile("" : "+v"(q0), "+v"(q1));
+      if constexpr (mode == kModeSstSeal) {
+        paux0 = *reinterpret_cast<gptr_u8>(q0);
+      } else if constexpr (mode == kModeVerify) {
+        paux0 = *reinterpret_cast<gptr_u32>(q0);
+      } else if constexpr (mode == kModeSstVerify || mode == kModeLogVerify) {
+        paux0 = *reinterpret_cast<gptr_u32>(q0);
+        paux1 = *reinterpret_cast<gptr_u32>(q1);
+      }
+    }
     rj = rn;
     ivj = ivn;
     cur_b = nb;
     cur_o = no;
   }
   retire();
-}
-
-// One thread per block: acc -> CRC -> output mode.
-__global__ __launch_bounds__(256) void crc32c_finish_kernel(RaggedArgs args) {
-  const DevConsts* __restrict__ dc = args.dc;
-  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < args.n;
-       b += (uint64_t)gridDim.x * blockDim.x) {
-    const ExtRaw raw = load_ext_raw(args, b);
-    uint64_t s0, e0;
-    extent_from_raw(args, b, raw, s0, e0);
-    const Frame f = frame_of(s0, e0);
-    const uint32_t z = (uint32_t)((f.row0 + f.rows) * kRowBytes - f.e);
-#ifdef LSBM_DEBUG_BOUNDS
-    if (z >= 128) { printf("Z OOB b %lu z %u s %lx e %lx row0 %lx rows %lu\n", (unsigned long)b, z, (unsigned long)f.s, (unsigned long)f.e, (unsigned long)f.row0, (unsigned long)f.rows); continue; }
-#endif
-    uint32_t l = nib_glb(dc->neg_nib[z], args.acc[b]);  // register after the block
-    if (args.mode == kModeSstSeal) {
-      const uint8_t typ = args.types[b];
-      l = dc->t0[(l ^ typ) & 0xffu] ^ (l >> 8);  // Extend(crc, &type, 1)
-    }
-    const uint32_t crc = l ^ 0xffffffffu;
-    switch (args.mode) {
-      case kModeOut:
-        args.out[b] = (args.flags & 1u) ? mask_crc(crc) : crc;
-        break;
-      case kModeVerify: {
-        const uint32_t got = (args.flags & 1u) ? mask_crc(crc) : crc;
-        const bool good = got == args.expect[b];
-        args.ok[b] = good ? 1 : 0;
-        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-        break;
-      }
-      case kModeSstSeal: {  // table/table_builder.cc:245-249
-        uint8_t* t = args.file + (f.e - reinterpret_cast<uint64_t>(args.base));
-        const uint32_t m = mask_crc(crc);
-        t[0] = args.types[b];
-        t[1] = (uint8_t)m;
-        t[2] = (uint8_t)(m >> 8);
-        t[3] = (uint8_t)(m >> 16);
-        t[4] = (uint8_t)(m >> 24);
-        break;
-      }
-      case kModeLogSeal: {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
-        if (!log_record_fits(args, raw)) {
-          if (args.out) args.out[b] = 0;
-          if (args.nbad) atomicAdd(args.nbad, 1u);
-          break;
-        }
-        uint8_t* h = args.file + raw.x;
-        const uint32_t m = mask_crc(crc);
-        h[0] = (uint8_t)m;
-        h[1] = (uint8_t)(m >> 8);
-        h[2] = (uint8_t)(m >> 16);
-        h[3] = (uint8_t)(m >> 24);
-        if (args.out) args.out[b] = m;
-        break;
-      }
-      case kModeLogVerify: {  // log::Reader::ReadPhysicalRecord, common/log_reader.cc:228-242
-        bool good = false;
-        if (log_record_fits(args, raw)) {
-          const uint8_t* h = args.base + raw.x;
-          const uint32_t stored = (uint32_t)h[0] | ((uint32_t)h[1] << 8) |
-                                  ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
-          good = unmask_crc(stored) == crc;
-        }
-        args.ok[b] = good ? 1 : 0;
-        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-        break;
-      }
-      default: {  // kModeSstVerify: table/format.cc:95-103
-        const uint8_t* t = reinterpret_cast<const uint8_t*>(f.e);
-        const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) |
-                                ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
-        const bool good = unmask_crc(stored) == crc;
-        args.ok[b] = good ? 1 : 0;
-        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-        break;
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -784,17 +835,36 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
   return hipGetLastError();
 }
 
-// acc must hold n zeroed words.
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
-  if (a.mode == kModeSstSeal || a.mode == kModeSstVerify)
-    hipLaunchKernelGGL(crc32c_units_kernel<kSstUnitRows>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
-  else
-    hipLaunchKernelGGL(crc32c_units_kernel<LSBM_UNIT_ROWS>, dim3(grid), dim3(kBlockThreads), 0, stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const uint64_t fin_wgs = (a.n + 255) / 256;
-  hipLaunchKernelGGL(crc32c_finish_kernel, dim3((unsigned)(fin_wgs < 65536 ? fin_wgs : 65536)),
-                     dim3(256), 0, stream, a);
+#define LSBM_LAUNCH_UNITS(R, M, X) \
+  hipLaunchKernelGGL((crc32c_units_kernel<R, M, X>), dim3(grid), dim3(kBlockThreads), 0, stream, a)
+  switch (a.mode) {
+    case kModeOut:
+      if (a.extents == kExtOffsets) LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeOut, kExtOffsets);
+      else if (a.extents == kExtHandles) LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeOut, kExtHandles);
+      else if (a.extents == kExtFixed) LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeOut, kExtFixed);
+      else return hipErrorInvalidValue;
+      break;
+    case kModeVerify:
+      if (a.extents != kExtOffsets) return hipErrorInvalidValue;
+      LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeVerify, kExtOffsets);
+      break;
+    case kModeSstSeal:
+      LSBM_LAUNCH_UNITS(kSstUnitRows, kModeSstSeal, kExtHandles);
+      break;
+    case kModeSstVerify:
+      LSBM_LAUNCH_UNITS(kSstUnitRows, kModeSstVerify, kExtHandles);
+      break;
+    case kModeLogSeal:
+      LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeLogSeal, kExtLogHeaders);
+      break;
+    case kModeLogVerify:
+      LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeLogVerify, kExtLogHeaders);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef LSBM_LAUNCH_UNITS
   return hipGetLastError();
 }
 

@@ -23,6 +23,9 @@ constexpr uint32_t kNibNeg4 = kNibRowPow + kRowPowTables * 512;  // A^-4 (init i
 constexpr uint32_t kLdsBytes = kNibNeg4 + 512;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
+constexpr uint32_t kShiftCols = 512;  // unit shifts up to 511 rows (64 KiB frames) by columns
+constexpr uint32_t kFinCols = 129;    // A^-z (z < 128) and A^(1 - z) (type-byte extension)
+
 // Tables in device global memory, built once per device by the host (gf2.h).
 struct DevConsts {
   uint32_t row_byte[4 * 256];    // byte tables of A^128 (main step)
@@ -31,6 +34,11 @@ struct DevConsts {
   uint32_t neg_nib[128][128];    // nibble tables of A^-z, z = 0..127
   uint32_t neg4_nib[128];        // nibble tables of A^-4
   uint32_t fin_nib[8][128];      // nibble tables of A^(116 - 16 li), li = 0..7 (merge)
+  // Column form (col[i] = M(1 << i)) of the matrices the units kernel applies
+  // once per unit / per block: an 8-lane group loads one matrix with one 16-B
+  // load per lane, issued a round ahead of its use (crc32c_kernels.hip).
+  alignas(16) uint32_t shift_cols[kShiftCols][32];  // A^(128 k), k < kShiftCols rows
+  alignas(16) uint32_t fin_cols[kFinCols][32];      // A^(e), e = -127 .. 1 (index e + 127)
   // The kernels' LDS image, prebuilt by the host so that each workgroup
   // fills its LDS with ~9 coalesced 16-B loads per thread.
   alignas(16) uint32_t lds_image[kLdsWords];
@@ -49,8 +57,10 @@ enum ExtentKind : uint32_t {
 enum RaggedMode : uint32_t {
   kModeOut = 0,        // out[i] = crc (masked if flags & 1)
   kModeVerify = 1,     // ok[i] = (crc == expect[i]); mismatches added to *nbad
-  kModeSstSeal = 2,    // write trailer [type][Mask(crc(block || type))] after the block
-  kModeSstVerify = 3,  // ok[i] = stored trailer == Mask(crc(block || type))
+  kModeSstSeal = 2,    // write trailer [type][Mask(crc(block || type))] after the block;
+                       // handles past `limit` (n + 5 bytes must fit) are counted, not written
+  kModeSstVerify = 3,  // ok[i] = stored trailer == Mask(crc(block || type)); handles past
+                       // `limit` are not ok (ReadBlock's "truncated block read")
   kModeLogSeal = 4,    // header[0..4) = Mask(crc(type || payload)); out[i] too if non-null
   kModeLogVerify = 5,  // ok[i] = Unmask(header[0..4)) == crc(type || payload)
 };
@@ -58,7 +68,9 @@ enum RaggedMode : uint32_t {
 // Ragged path: a block's 128-B-aligned frame [row0, row_end) of R rows is cut
 // into m = ceil(R / kUnitRows) units of near-equal size (R / m rows, the first
 // R % m of them one more).  A unit's raw CRC is shifted to the frame end with
-// A^(128 k), k = the frame's rows after the unit.
+// A^(128 k), k = the frame's rows after the unit; the units of a block are
+// summed inside the wave (crc32c_kernels.hip) and the block is finished by the
+// lane group holding its last unit.
 constexpr uint32_t kUnitRows = 48;  // A/B 24..96 rows: plateau from 48
 constexpr uint32_t kSstUnitRows = 40;  // SSTable trailer modes: a ~4 KiB block is one unit
 
@@ -79,9 +91,9 @@ struct RaggedArgs {
   uint32_t mode;
   uint32_t extents;
   const DevConsts* dc;
-  uint32_t* acc;         // n per-block accumulators (zeroed before the units kernel)
-  uint64_t limit;        // kExtLogHeaders: image size; records past it are empty + bad
-  uint64_t dbg_lo, dbg_hi;  // LSBM_DEBUG_BOUNDS builds: the valid data range
+  uint32_t u_noinit;     // A^-4(~0): the virtual init bytes when init == nullptr
+  uint64_t limit;        // kExtLogHeaders / SST modes: image size; records past it are
+                         // empty + bad (~0 = unbounded)
 };
 
 }  // namespace lsbm

@@ -83,7 +83,7 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
   DeviceBuffers d;
   s = stage(device, file, file_size, handles, n, types, &d);
   if (!s.ok()) return s;
-  if (lsbm_sst_seal_dev(d.file, d.handles, d.aux, n, d.stream.get()) != LSBM_OK)
+  if (lsbm_sst_seal_dev(d.file, file_size, d.handles, d.aux, n, nullptr, d.stream.get()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
   // Bring the image back whole through the pinned bounce: one streamed copy
   // instead of one 5-byte hipMemcpyAsync (a runtime call) per block.  The
@@ -103,7 +103,7 @@ Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockH
   DeviceBuffers d;
   s = stage(device, file, file_size, handles, n, nullptr, &d);
   if (!s.ok()) return s;
-  if (lsbm_sst_verify_dev(d.file, d.handles, n, d.aux, d.nbad, d.stream.get()) != LSBM_OK)
+  if (lsbm_sst_verify_dev(d.file, file_size, d.handles, n, d.aux, d.nbad, d.stream.get()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
   uint32_t nbad = 0;
   hipError_t e = d.bounce.to_host(&nbad, d.nbad, sizeof(nbad), d.stream.get());

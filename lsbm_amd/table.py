@@ -64,23 +64,43 @@ def layout_blocks(sizes):
     return handles, total
 
 
-def seal_blocks(file_image, handles, types, stream=None):
-    """Batched WriteRawBlock trailers: writes file_image[off+size : off+size+5]."""
+def _check_image(file_image, handles, types=None):
+    torch = _torch()
     _require_cuda(file_image, handles, types)
+    if file_image.dtype != torch.uint8 or not file_image.is_contiguous():
+        raise ValueError("file_image must be a contiguous uint8 tensor")
+    if handles.dtype != torch.int64 or handles.numel() % 2 or not handles.is_contiguous():
+        raise ValueError("handles must be contiguous int64 {offset, size} pairs")
     n = handles.numel() // 2
-    check(lib().lsbm_sst_seal_dev(_ptr(file_image), _ptr(handles), _ptr(types), n,
-                                  _stream_ptr(stream)), "lsbm_sst_seal_dev")
+    if types is not None and (types.dtype != torch.uint8 or types.numel() < n):
+        raise ValueError("types must be uint8 with one entry per block")
+    return n
+
+
+def seal_blocks(file_image, handles, types, stream=None, nbad=None):
+    """Batched WriteRawBlock trailers: writes file_image[off+size : off+size+5].
+    Handles whose size + 5 bytes fall outside the image are left alone and
+    counted into `nbad` (int32[1], returned; created when None)."""
+    torch = _torch()
+    n = _check_image(file_image, handles, types)
+    if nbad is None:
+        nbad = torch.zeros(1, dtype=torch.int32, device=file_image.device)
+    check(lib().lsbm_sst_seal_dev(_ptr(file_image), file_image.numel(), _ptr(handles),
+                                  _ptr(types), n, _ptr(nbad), _stream_ptr(stream)),
+          "lsbm_sst_seal_dev")
+    return nbad
 
 
 def verify_blocks(file_image, handles, stream=None):
-    """Batched ReadBlock verify: returns (ok uint8[n], nbad int32[1])."""
+    """Batched ReadBlock verify: returns (ok uint8[n], nbad int32[1]).  A
+    handle past the image (truncated block read) is not ok."""
     torch = _torch()
-    _require_cuda(file_image, handles)
-    n = handles.numel() // 2
+    n = _check_image(file_image, handles)
     ok = torch.empty(n, dtype=torch.uint8, device=file_image.device)
     nbad = torch.zeros(1, dtype=torch.int32, device=file_image.device)
-    check(lib().lsbm_sst_verify_dev(_ptr(file_image), _ptr(handles), n, _ptr(ok), _ptr(nbad),
-                                    _stream_ptr(stream)), "lsbm_sst_verify_dev")
+    check(lib().lsbm_sst_verify_dev(_ptr(file_image), file_image.numel(), _ptr(handles), n,
+                                    _ptr(ok), _ptr(nbad), _stream_ptr(stream)),
+          "lsbm_sst_verify_dev")
     return ok, nbad
 
 

@@ -241,7 +241,8 @@ def _config_fixed(torch, oracle, golden, name, seed, L, n, check_ragged_blocks):
     offs = torch.arange(0, (m + 1) * L, L, dtype=torch.int64, device="cuda")
     other = engine.crc32c_batch(d, offs)
     assert torch.equal(other, crc[:m])
-    del d
+    del d, crc, other, offs
+    torch.cuda.empty_cache()
 
 
 def test_config2_full_1M_x_4KiB(torch_cuda, oracle, golden):
@@ -329,3 +330,176 @@ def test_fixed_batch_replays_in_a_hip_graph(torch_cuda, oracle):
     torch.cuda.synchronize()
     want2 = oracle.batch_fixed(stream_bytes(0xABD, 0, n * L), L, L, n)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want2)
+
+
+# ---------------------------------------------------------------- ragged path extras
+def test_ragged_huge_blocks_and_carries(torch_cuda, oracle):
+    """Blocks of 0 B .. 3 MiB mixed, so that a block's units span many rounds
+    (in-wave carries) and unit shifts exceed the 512-row column tables."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    rng = np.random.default_rng(101)
+    lens = np.concatenate([rng.integers(0, 300, 40), [3 << 20, 0, 1, 200000, 65536, 65537],
+                           rng.integers(0, 9000, 60), [1 << 20, 129, 128, 127]])
+    rng.shuffle(lens)
+    offs = np.zeros(lens.size + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    offs += 3
+    data = stream_bytes(101, 0, int(offs[-1]) + 16)
+    init = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    for use_init in (False, True):
+        got = _u32(engine.crc32c_batch(_dev(torch, data), _dev(torch, offs),
+                                       init=_dev(torch, init, torch.int32) if use_init else None))
+        want = oracle.batch_offsets(data, offs.astype(np.uint64), init if use_init else None)
+        assert np.array_equal(got, want)
+
+
+def test_ragged_batch_replays_in_a_hip_graph(torch_cuda, oracle):
+    """The ragged path is one launch with no allocation, so it is capturable."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    starts, ends, total = _ragged_case(55, 3000, 9000)
+    offs = _dev(torch, np.concatenate([starts, ends[-1:]]).astype(np.int64))
+    d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 0xAB0)
+    out = torch.zeros(3000, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        engine.crc32c_batch(d, offs, out=out, masked=True, stream=torch.cuda.current_stream())
+    for seed in (0xAB0, 0xAB1):
+        engine.fill_splitmix64(d, seed)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        want = oracle.batch_offsets(stream_bytes(seed, 0, total + 16),
+                                    offs.cpu().numpy().astype(np.uint64), masked=True)
+        assert np.array_equal(_u32(out), want)
+
+
+# ---------------------------------------------------------------- config 4 (full size)
+def test_config4_full_10M_zipf(torch_cuda, oracle):
+    """BASELINE.json configs[3]: 10M blocks, n = min(65536, 512 r + u), r ~ Zipf(0.99),
+    densely packed from an odd start (117 GiB: extents cross 4 GiB multiples and
+    2^36).  Checked block-for-block against the oracle on >= 4,096 blocks: every
+    block crossing a 4 GiB multiple, the first and last 64, and a random sample;
+    plus verify mode over the whole batch against the computed CRCs."""
+    torch = torch_cuda
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    from bench_configs import zipf_lengths
+    from lsbm_amd import engine
+    n, seed, pad = 10_000_000, 0x5EED0003, 5
+    lens = zipf_lengths(n)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    offs += pad
+    total = int(offs[-1]) + 16
+    assert total > (1 << 36)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, seed)
+    do = _dev(torch, offs)
+    crc = engine.crc32c_batch(d, do)
+    got = _u32(crc)
+    cross = np.nonzero((offs[:-1] >> 32) != ((offs[1:] - 1) >> 32))[0]
+    cross36 = np.nonzero((offs[:-1] >> 36) != ((offs[1:] - 1) >> 36))[0]
+    assert cross.size >= 20 and cross36.size >= 1
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([cross, cross36, np.arange(64), np.arange(n - 64, n),
+                                    rng.choice(n, 4096, replace=False)]))
+    assert idx.size >= 4096
+    for b in idx:
+        blk = stream_bytes(seed, int(offs[b]), int(lens[b])).tobytes()
+        assert got[b] == oracle.value(blk), int(b)
+    ok, nbad = engine.crc32c_verify(d, do, crc)
+    assert int(nbad.item()) == 0 and bool(ok.all())
+    del d, do, crc, ok
+    torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------- SSTable at real scale
+def test_sst_1M_x_4118_seal_verify_roundtrip(torch_cuda, oracle):
+    """1M real-size data blocks (4,118 B) laid out as a file image
+    with trailers: lsbm_sst_seal_dev writes every trailer, sampled trailers equal
+    the oracle's Mask(Extend(Value(block), type)), lsbm_sst_verify_dev passes all,
+    then single-byte corruptions of payload, type and crc fail exactly those blocks."""
+    torch = torch_cuda
+    from lsbm_amd import table
+    n, L, seed = 1 << 20, 4118, 0x5EED0005
+    sizes = np.full(n, L, dtype=np.int64)
+    handles, total = table.layout_blocks(sizes)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine_fill(d, seed)
+    rng = np.random.default_rng(7)
+    types = rng.integers(0, 2, n).astype(np.uint8)
+    dh = _dev(torch, handles.astype(np.int64))
+    nbad = table.seal_blocks(d, dh, _dev(torch, types))
+    assert int(nbad.item()) == 0
+    sample = np.unique(np.concatenate([np.arange(32), np.arange(n - 32, n),
+                                       rng.choice(n, 4096, replace=False)]))
+    img = d.cpu().numpy()
+    for i in sample:
+        off = int(handles[2 * i])
+        blk = stream_bytes(seed, off, L).tobytes()
+        assert img[off:off + L].tobytes() == blk
+        crc = oracle.extend(oracle.value(blk), bytes([types[i]]))
+        assert img[off + L] == types[i]
+        assert int.from_bytes(img[off + L + 1:off + L + 5].tobytes(), "little") == oracle.mask(crc), i
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == 0 and bool(ok.all())
+    bad = rng.choice(n, 30, replace=False)
+    for j, i in enumerate(bad):
+        off = int(handles[2 * i])
+        pos = off + (int(rng.integers(0, L)) if j % 3 == 0 else (L if j % 3 == 1 else L + 1 + j % 4))
+        d[pos] ^= 1 << (j % 8)
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == bad.size
+    assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(bad.tolist())
+    del d
+    torch.cuda.empty_cache()
+
+
+def engine_fill(d, seed):
+    from lsbm_amd import engine
+    engine.fill_splitmix64(d, seed)
+
+
+def test_sst_handles_past_the_image(torch_cuda, oracle):
+    """ReadBlock's "truncated block read" (table/format.cc:88-91) on the device
+    ABI: a handle whose n + 5 bytes leave the image is never read or written,
+    is counted, and is not ok; every other block is sealed and verified."""
+    torch = torch_cuda
+    from lsbm_amd import table
+    rng = np.random.default_rng(12)
+    sizes = rng.integers(0, 6000, 200)
+    handles, total = table.layout_blocks(sizes)
+    handles = handles.astype(np.int64).copy()
+    img = stream_bytes(12, 0, total)
+    # guard bytes after the image: must stay untouched
+    guard = np.full(4096, 0xA5, dtype=np.uint8)
+    full = np.concatenate([img, guard])
+    d_full = _dev(torch, full)
+    d = d_full[:total]
+    bad = {3: (total - 2, 0), 17: (total - 10, 6), 50: (total + 100, 1), 51: (2**62, 10),
+           77: (int(handles[2 * 77]), total)}
+    for i, (o, sz) in bad.items():
+        handles[2 * i], handles[2 * i + 1] = o, sz
+    # the last block ends exactly at the image end: fits
+    dh = _dev(torch, handles)
+    types = rng.integers(0, 2, sizes.size).astype(np.uint8)
+    nbad = table.seal_blocks(d, dh, _dev(torch, types))
+    assert int(nbad.item()) == len(bad)
+    out = d_full.cpu().numpy()
+    assert np.array_equal(out[total:], guard)
+    for i in range(sizes.size):
+        if i in bad:
+            continue
+        off, sz = int(handles[2 * i]), int(sizes[i])
+        crc = oracle.extend(oracle.value(out[off:off + sz].tobytes()), bytes([types[i]]))
+        assert int.from_bytes(out[off + sz + 1:off + sz + 5].tobytes(), "little") == oracle.mask(crc)
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == len(bad)
+    assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(bad)

@@ -1,0 +1,57 @@
+"""bench.py's N > 1 path on the one-GPU box: `python bench.py --gpus 2` starts
+its own two ranks (torch.distributed.run as a child process), each rank
+checksums its own config-5-shaped shard (10M x 4 KiB blocks, BASELINE.json
+configs[4]) on the HIP path, and the per-rank results are checked here against
+the oracle.  Both ranks share the one MI355X (LSBM_BENCH_DEVICES=1) and meet
+over gloo (LSBM_BENCH_BACKEND=gloo); the driver's 8-GPU run uses RCCL."""
+import glob
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from golden.splitmix import stream_bytes
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(LSBM_BENCH_DEVICES="1", LSBM_BENCH_BACKEND="gloo")
+    prefix = str(tmp_path / "samples")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                        "--dump-samples", prefix],
+                       env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["blocks_per_gpu"] == 10_000_000
+    files = sorted(glob.glob(prefix + ".rank*.npz"))
+    assert len(files) == 2
+    seeds = set()
+    for f in files:
+        z = np.load(f)
+        assert int(z["world"]) == 2 and int(z["n"]) == 10_000_000
+        seed = int(z["seed"])
+        seeds.add(seed)
+        for i, c in zip(z["idx"], z["crc"]):
+            assert c == oracle.value(stream_bytes(seed, int(i) * 4096, 4096).tobytes()), (f, int(i))
+    assert len(seeds) == 2  # each rank generated and checksummed its own shard
+
+
+def test_bench_rejects_world_size_mismatch():
+    """WORLD_SIZE set by a launcher but != --gpus is an error, not a warning
+    (exits before any GPU call, so this runs on CPU)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 2
+    assert "WORLD_SIZE" in r.stderr
