@@ -9,7 +9,7 @@
 //                 the GPU (lsbm_log_seal_dev).  This is a group commit: many
 //                 AddRecord calls, one CRC batch.
 //   ReadLog       what DBImpl::RecoverLogFile / VersionSet::Recover get from
-//                 log::Reader(file, reporter, checksum=true, initial_offset=0)
+//                 log::Reader(file, reporter, checksum=true, initial_offset)
 //                 (lsbm/db_impl.cc:428, lsbm/version_set.cc:2026): the same
 //                 records in the same order and the same Reporter::Corruption
 //                 calls (bytes, status), with every physical record's
@@ -79,16 +79,19 @@ class Reporter {
 };
 
 // log::Reader (common/log_reader.h:20-103) over an in-memory log file image
-// file[0, n), with checksum = true and initial_offset = 0 (the only
-// configuration lsbm's recovery uses: lsbm/db_impl.cc:428,
-// lsbm/version_set.cc:2026).  Verify() checks every physical record's CRC in
-// one GPU batch; ReadRecord() then returns the same records, with the same
+// file[0, n), with checksum = true.  lsbm's recovery reads from offset 0
+// (lsbm/db_impl.cc:428, lsbm/version_set.cc:2026); a non-zero initial_offset
+// behaves as the reference's: reading starts at the block holding it
+// (SkipToInitialBlock, common/log_reader.cc:35-57), physical records that
+// begin before it are skipped, and drops before it are not reported
+// (:171-176, :247-251).  Verify() checks every physical record's CRC in one
+// GPU batch; ReadRecord() then returns the same records, with the same
 // LastRecordOffset() and the same reporter->Corruption calls, in the same
 // order as the reference reader.  `file` and `reporter` must outlive it.
 class Walk;
 class BatchReader {
  public:
-  BatchReader(const char* file, size_t n, Reporter* reporter);
+  BatchReader(const char* file, size_t n, Reporter* reporter, uint64_t initial_offset = 0);
   ~BatchReader();
 
   // The GPU batch (lsbm_log_verify_dev).  Must precede ReadRecord; a non-OK
@@ -106,6 +109,7 @@ class BatchReader {
   const char* file_;
   size_t size_;
   Reporter* reporter_;
+  uint64_t initial_offset_;
   std::vector<uint64_t> headers_;  // every header the reader may check
   std::vector<uint8_t> ok_;        // their CRC verdicts
   Walk* walk_;
@@ -115,7 +119,8 @@ class BatchReader {
 // Convenience: every record of the image (and its offset), as a recovery
 // loop over BatchReader::ReadRecord collects them.
 Status ReadLog(int device, const char* file, size_t n, Reporter* reporter,
-               std::vector<std::string>* records, std::vector<uint64_t>* offsets);
+               std::vector<std::string>* records, std::vector<uint64_t>* offsets,
+               uint64_t initial_offset = 0);
 
 }  // namespace log
 }  // namespace lsbm

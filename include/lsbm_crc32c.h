@@ -106,6 +106,15 @@ int lsbm_crc32c_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64
  * type = d_types[i] (CompressionType, include/leveldb/options.h:24-29). */
 int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
                       const uint8_t* d_types, uint64_t n_blocks, uint32_t* d_nbad, void* stream);
+/* The same trailers without touching the image: d_masked[i] =
+ * Mask(Extend(Value(block i), &d_types[i], 1)), the 4 bytes WriteRawBlock
+ * stores after the type byte (0 for a handle past the image, counted into
+ * *d_nbad).  The output is dense, 4 B per block: scattered 5-byte writes into
+ * the image cost the memory system more than the whole CRC read (DESIGN.md
+ * section 3), so a host that writes the file itself wants this one. */
+int lsbm_sst_trailer_crcs_dev(const uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
+                              const uint8_t* d_types, uint64_t n_blocks, uint32_t* d_masked,
+                              uint32_t* d_nbad, void* stream);
 /* ReadBlock verify (table/format.cc:95-103): d_ok[i] = 1 iff the block fits and
  * Unmask(DecodeFixed32(trailer+1)) == Value(block || type); failures are
  * added to *d_nbad when non-NULL. */

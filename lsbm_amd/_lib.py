@@ -41,6 +41,7 @@ SIGNATURES = {
     "lsbm_crc32c_verify_dev": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp]),
     "lsbm_sst_seal_dev": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     "lsbm_sst_verify_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "lsbm_sst_trailer_crcs_dev": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_log_seal_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_log_verify_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_crc32c_batch_host": (_int, [_int, _vp, _vp, _u64, _vp, _vp, _u32]),

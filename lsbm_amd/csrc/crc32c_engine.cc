@@ -427,6 +427,24 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
+__attribute__((visibility("default"))) int lsbm_sst_trailer_crcs_dev(
+    const uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles, const uint8_t* d_types,
+    uint64_t n_blocks, uint32_t* d_masked, uint32_t* d_nbad, void* stream) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!d_file || !d_handles || !d_types || !d_masked) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_file;
+  a.handles = d_handles;
+  a.extents = kExtHandles;
+  a.types = d_types;
+  a.n = n_blocks;
+  a.out = d_masked;
+  a.nbad = d_nbad;
+  a.limit = file_bytes;
+  a.mode = kModeSstCrc;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
 __attribute__((visibility("default"))) int lsbm_sst_verify_dev(const uint8_t* d_file,
                                                                uint64_t file_bytes,
                                                                const uint64_t* d_handles,

@@ -280,7 +280,7 @@ __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b,
     e = fits ? s + 1 + r.y : s;
     at = base + r.x;
   } else if (a.extents == kExtHandles) {
-    if (a.mode == kModeSstSeal || a.mode == kModeSstVerify)
+    if (a.mode == kModeSstSeal || a.mode == kModeSstVerify || a.mode == kModeSstCrc)
       fits = r.x <= a.limit && a.limit - r.x >= kTrailer && a.limit - r.x - kTrailer >= r.y;
     s = base + (fits ? r.x : 0);
     e = fits ? s + r.y + (a.mode == kModeSstVerify ? 1u : 0u) : s;  // verify covers the type
@@ -394,11 +394,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   const uint32_t* __restrict__ init = args.init;
   constexpr uint32_t mode = kMode;
   const uint32_t jl = lane < 8u ? lane : 8u;  // lanes 0..8 hold the walk's 9 blocks
-  // extents (+ init) of blocks nb + jl, clamped into the range so that the
-  // loads are unconditional; only lanes with nb + lane < b_hi use them
+  // extents (+ init) of blocks nb + jl, clamped into the batch so that the
+  // loads are unconditional; only lanes with nb + lane < b_hi walk them
   auto prefetch = [&](uint64_t nb, ExtRaw& r, uint32_t& iv) {
     uint64_t idx = nb + jl;
-    idx = idx < b_hi ? idx : b_hi - 1;
+    idx = idx < args.n ? idx : args.n - 1;
     r = load_ext_raw(args, idx);
     iv = init ? reinterpret_cast<gptr_u32>(reinterpret_cast<uint64_t>(init))[idx] : 0u;
   };
@@ -422,6 +422,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   uint64_t pk = 0, pb = 0, pat = 0;
   bool pact = false, plast = false, pfits = true;
 
+  uint64_t pend_a = 0;  // this lane's parked result (0 = none), see retire()
+  uint32_t pend_v = 0, pend_i = 0;
+  uint32_t round = 0;   // rounds retired so far (wave-uniform)
   auto retire = [&]() {
     const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
     uint32_t v = cols_apply(pshift, raw, li);        // A^(128 (k mod 512))
@@ -443,8 +446,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     carry_v = __builtin_amdgcn_readlane(v, 56);
     carry_b = (key7 != ~0ull && !last7) ? key7 : ~0ull;
     // finish: register after the block = A^-z(v) (A^(1-z) for the seal's type byte)
-    uint32_t l = cols_apply(pfin, v, li);
+    const uint32_t l = cols_apply(pfin, v, li);
+    const uint32_t crc = l ^ 0xffffffffu;
+    // The finishing group's result is parked in ONE lane of the group, the
+    // lane whose index is the round number mod 8, and written by
+    // flush_stores() once every 8 rounds: stores count in the same in-order
+    // vmcnt queue as loads, and a store in front of row loads delays every
+    // wait for those rows until it is acknowledged (~3,000 cycles with every
+    // CU streaming), so one flush per 8 rounds instead of a store per round.
     if (!(pact && plast)) return;
+    const bool mine = li == (round & 7u);
     if constexpr (mode == kModeSstSeal) {  // table/table_builder.cc:245-249
       if (!pfits) {
         if (li == 0 && args.nbad) atomicAdd(args.nbad, 1u);
@@ -452,45 +463,93 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       }
       const uint32_t typ = paux0 & 0xffu;
       const uint32_t m = mask_crc((l ^ advance_byte(typ)) ^ 0xffffffffu);  // Extend(crc, &type, 1)
-      if (li < kTrailer)  // [type][masked crc LE32], one byte per lane
+      // the trailer [type][masked crc LE32] at pat, one byte per lane.  These
+      // scattered writes cost ~13% of HBM peak (A/B: the same 4-byte writes
+      // added to verify took it from 75% to 62%; whole 64-B line writes were
+      // no better): lsbm_sst_trailer_crcs_dev returns dense CRCs instead.
+      if (li < kTrailer)
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(li == 0 ? typ : m >> (8 * (li - 1)));
-      return;
+    } else if constexpr (mode == kModeSstCrc) {  // the same crc, dense: out[b]
+      const uint32_t typ = paux0 & 0xffu;
+      if (!pfits && li == 0 && args.nbad) atomicAdd(args.nbad, 1u);
+      if (mine) {
+        pend_a = reinterpret_cast<uint64_t>(args.out + pb);
+        pend_v = pfits ? mask_crc((l ^ advance_byte(typ)) ^ 0xffffffffu) : 0u;
+      }
+    } else if constexpr (mode == kModeLogSeal) {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
+      if (!pfits && li == 0) {
+        if (args.out) args.out[pb] = 0;
+        if (args.nbad) atomicAdd(args.nbad, 1u);
+      }
+      if (pfits && mine) {  // header[0..4) at pat (+ out[pb] when requested)
+        pend_a = pat;
+        pend_v = mask_crc(crc);
+        pend_i = (uint32_t)(pb - b_lo);
+      }
+    } else if constexpr (mode == kModeOut) {
+      if (mine) {
+        pend_a = reinterpret_cast<uint64_t>(args.out + pb);
+        pend_v = (args.flags & 1u) ? mask_crc(crc) : crc;
+      }
+    } else {
+      bool good;
+      if constexpr (mode == kModeVerify)
+        good = ((args.flags & 1u) ? mask_crc(crc) : crc) == paux0;
+      else  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+        good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
+#ifdef LSBM_DIAG_VERIFY_WRITEBACK  // diagnostic builds only: rewrite the stored crc bytes
+      if (pfits && li < 4)
+        reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(unaligned_word(paux0, paux1, pat) >> (8 * li));
+#endif
+#ifdef LSBM_DIAG_VERIFY_WRITEBACK_DW  // diagnostic builds only: rewrite the covering dwords
+      if (pfits && li == 0) {
+        reinterpret_cast<uint32_t*>(pat & ~3ull)[0] = paux0;
+        reinterpret_cast<uint32_t*>((pat + 3) & ~3ull)[0] = paux1;
+      }
+#endif
+#ifdef LSBM_DIAG_VERIFY_WRITEBACK_64  // diagnostic builds only: rewrite the covering 64-B line
+      if (pfits && li < 4) {
+        u32x4* q = reinterpret_cast<u32x4*>((pat & ~63ull) + 16 * li);
+        const u32x4 v = *q;
+        *q = v;
+      }
+#endif
+      if (mine) {
+        pend_a = reinterpret_cast<uint64_t>(args.ok + pb);
+        pend_v = good ? 1u : 0u;
+      }
+      if (!good && li == 0 && args.nbad) atomicAdd(args.nbad, 1u);
     }
-    if (li != 0) return;
-    const uint32_t crc = l ^ 0xffffffffu;
-    switch (mode) {
-      case kModeOut:
-        args.out[pb] = (args.flags & 1u) ? mask_crc(crc) : crc;
-        break;
-      case kModeVerify: {
-        const uint32_t got = (args.flags & 1u) ? mask_crc(crc) : crc;
-        const bool good = got == paux0;
-        args.ok[pb] = good ? 1 : 0;
-        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-        break;
-      }
-      case kModeLogSeal: {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
-        if (!pfits) {
-          if (args.out) args.out[pb] = 0;
-          if (args.nbad) atomicAdd(args.nbad, 1u);
-          break;
-        }
-        uint8_t* h = reinterpret_cast<uint8_t*>(pat);
-        const uint32_t m = mask_crc(crc);
-        h[0] = (uint8_t)m;
-        h[1] = (uint8_t)(m >> 8);
-        h[2] = (uint8_t)(m >> 16);
-        h[3] = (uint8_t)(m >> 24);
-        if (args.out) args.out[pb] = m;
-        break;
-      }
-      default: {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
-        const bool good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
-        args.ok[pb] = good ? 1 : 0;
-        if (!good && args.nbad) atomicAdd(args.nbad, 1u);
-        break;
+  };
+  auto flush_stores = [&]() {
+#ifndef LSBM_DIAG_NO_STORE  // diagnostic builds only: results not written
+    if (pend_a) {
+      if constexpr (mode == kModeSstSeal) {
+        uint8_t* t = reinterpret_cast<uint8_t*>(pend_a & 0x00ffffffffffffffull);
+        t[0] = (uint8_t)(pend_a >> 56);
+        t[1] = (uint8_t)pend_v;
+        t[2] = (uint8_t)(pend_v >> 8);
+        t[3] = (uint8_t)(pend_v >> 16);
+        t[4] = (uint8_t)(pend_v >> 24);
+      } else if constexpr (mode == kModeLogSeal) {
+        uint8_t* h = reinterpret_cast<uint8_t*>(pend_a);
+        h[0] = (uint8_t)pend_v;
+        h[1] = (uint8_t)(pend_v >> 8);
+        h[2] = (uint8_t)(pend_v >> 16);
+        h[3] = (uint8_t)(pend_v >> 24);
+        if (args.out) args.out[b_lo + pend_i] = pend_v;
+      } else if constexpr (mode == kModeOut || mode == kModeSstCrc) {
+#ifdef LSBM_DIAG_OUT_BYTE  // diagnostic builds only: one byte per block instead of a dword
+        reinterpret_cast<uint8_t*>(args.out)[(pend_a - reinterpret_cast<uint64_t>(args.out)) / 4] = (uint8_t)pend_v;
+#else
+        *reinterpret_cast<uint32_t*>(pend_a) = pend_v;
+#endif
+      } else {
+        *reinterpret_cast<uint8_t*>(pend_a) = (uint8_t)pend_v;
       }
     }
+#endif
+    pend_a = 0;
   };
 
   while (cur_b < b_hi) {
@@ -608,7 +667,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     // Until then only these compact words stay live across the row loop.
     const bool last = active && o + 1 == f.units;
     const uint32_t zf = (uint32_t)((f.row0 + f.rows) * kRowBytes - f.e);  // < 128
-    const uint32_t fin_i = active ? (mode == kModeSstSeal ? 128u : 127u) - zf : 127u;
+    const uint32_t fin_i = active ? (mode == kModeSstSeal || mode == kModeSstCrc ? 128u : 127u) - zf : 127u;
     const uint32_t st_i = (active ? (uint32_t)(k & (kShiftCols - 1)) : 0u) | (fin_i << 16) |
                           (last ? 1u << 24 : 0u) | (fits ? 1u << 25 : 0u) | (active ? 1u << 26 : 0u);
     const uint32_t b_rel = (uint32_t)(b - b_lo);  // a wave's range is < 2^32 blocks
@@ -648,6 +707,12 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint32_t u = (kExt != kExtLogHeaders && init) ? nib_lds_at(g_lds, kNibNeg4, iv ^ 0xffffffffu)  // A^-4(init ^ ~0)
                             : args.u_noinit;
     retire();
+#ifdef LSBM_FLUSH_EVERY_ROUND  // A/B builds only
+    flush_stores();
+#else
+    if ((round & 7u) == 7u) flush_stores();
+#endif
+    round++;
 
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
     auto absorb = [&](u32x4 w, uint32_t r) {  // rows read from the pad are zero
@@ -655,7 +720,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       // the (r < rows) branch, the vmcnt wait sat on that path alone, and the
       // next reload of the bank had to drain every load still in flight.
       asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+#ifdef LSBM_DIAG_NOGUARD  // diagnostic builds only (wrong CRCs): every row absorbed
+      STEP_ROW(w);
+#else
       if (r < rows) STEP_ROW(w);
+#endif
     };
     // The start fix (init bytes, bytes before s) only ever falls on rows 0
     // and 1 of a unit: chunk c of row 0 has c <= s - 4 and the fix chunk has
@@ -726,7 +795,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       uint64_t q0 = dummy, q1 = dummy;
       if constexpr (mode == kModeVerify) {
         q0 = need ? reinterpret_cast<uint64_t>(args.expect + pb) : dummy;
-      } else if constexpr (mode == kModeSstSeal) {
+      } else if constexpr (mode == kModeSstSeal || mode == kModeSstCrc) {
         q0 = need ? reinterpret_cast<uint64_t>(args.types + pb) : dummy;
       } else if constexpr (mode == kModeSstVerify || mode == kModeLogVerify) {
         // the dwords holding bytes pat and pat + 3 (one dword when aligned:
@@ -735,7 +804,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
         q1 = need ? ((pat + 3) & ~3ull) : dummy;
       }
       asm volatile("" : "+v"(q0), "+v"(q1));
-      if constexpr (mode == kModeSstSeal) {
+      if constexpr (mode == kModeSstSeal || mode == kModeSstCrc) {
         paux0 = *reinterpret_cast<gptr_u8>(q0);
       } else if constexpr (mode == kModeVerify) {
         paux0 = *reinterpret_cast<gptr_u32>(q0);
@@ -750,6 +819,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     cur_o = no;
   }
   retire();
+  flush_stores();
 }
 
 // ---------------------------------------------------------------------------
@@ -854,6 +924,9 @@ hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
       break;
     case kModeSstVerify:
       LSBM_LAUNCH_UNITS(kSstUnitRows, kModeSstVerify, kExtHandles);
+      break;
+    case kModeSstCrc:
+      LSBM_LAUNCH_UNITS(kSstUnitRows, kModeSstCrc, kExtHandles);
       break;
     case kModeLogSeal:
       LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeLogSeal, kExtLogHeaders);

@@ -63,6 +63,8 @@ enum RaggedMode : uint32_t {
                        // `limit` are not ok (ReadBlock's "truncated block read")
   kModeLogSeal = 4,    // header[0..4) = Mask(crc(type || payload)); out[i] too if non-null
   kModeLogVerify = 5,  // ok[i] = Unmask(header[0..4)) == crc(type || payload)
+  kModeSstCrc = 6,     // out[i] = Mask(crc(block || type)): the trailer's crc, dense (the
+                       // image is not written); handles past `limit` give 0 and are counted
 };
 
 // Ragged path: a block's 128-B-aligned frame [row0, row_end) of R rows is cut

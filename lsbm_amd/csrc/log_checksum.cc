@@ -66,19 +66,22 @@ enum : unsigned int { kEof = kMaxRecordType + 1, kBadRecord = kMaxRecordType + 2
 
 }  // namespace
 
-// One pass of log::Reader over an in-memory file (checksum = true,
-// initial_offset = 0).  In the collecting pass every header whose checksum
-// the reader would test is recorded and assumed good; in the replay pass the
-// GPU's verdicts are used and Reporter calls are made.
+// One pass of log::Reader over an in-memory file (checksum = true, any
+// initial_offset).  In the collecting pass every header whose checksum the
+// reader would test is recorded and assumed good; in the replay pass the
+// GPU's verdicts are used and Reporter calls are made.  The reader's buffer_
+// is file[buf_begin_, buf_end_) and buf_end_ is its end_of_buffer_offset_.
 class Walk {
  public:
-  Walk(const uint8_t* file, size_t size, Reporter* reporter, std::vector<uint64_t>* collect,
-       const std::vector<uint64_t>* checked, const std::vector<uint8_t>* ok)
+  Walk(const uint8_t* file, size_t size, uint64_t initial_offset, Reporter* reporter,
+       std::vector<uint64_t>* collect, const std::vector<uint64_t>* checked,
+       const std::vector<uint8_t>* ok)
       : file_(file), size_(size), reporter_(reporter), collect_(collect), checked_(checked),
-        ok_(ok) {}
+        ok_(ok), initial_offset_(initial_offset) {}
 
   // log::Reader::ReadRecord (common/log_reader.cc:59-162).
   bool ReadRecord(std::string* record, uint64_t* record_offset) {
+    if (last_record_offset_ < initial_offset_) SkipToInitialBlock();
     scratch_.clear();
     record->clear();
     bool in_fragmented_record = false;
@@ -92,7 +95,7 @@ class Walk {
           if (in_fragmented_record && !scratch_.empty())
             Report(scratch_.size(), "partial record without end(1)");
           record->assign(reinterpret_cast<const char*>(file_) + frag, frag_len);
-          *record_offset = physical_offset;
+          *record_offset = last_record_offset_ = physical_offset;
           return true;
         case kFirstType:
           if (in_fragmented_record && !scratch_.empty())
@@ -113,7 +116,7 @@ class Walk {
           } else {
             scratch_.append(reinterpret_cast<const char*>(file_) + frag, frag_len);
             record->swap(scratch_);
-            *record_offset = prospective_offset;
+            *record_offset = last_record_offset_ = prospective_offset;
             return true;
           }
           break;
@@ -142,18 +145,40 @@ class Walk {
     }
   }
 
+  uint64_t LastRecordOffset() const { return last_record_offset_; }
+
  private:
-  // log::Reader::ReadPhysicalRecord (common/log_reader.cc:179-256).  The
-  // buffer is file[buf_begin_, buf_end_); reads come in kBlockSize pieces.
+  // log::Reader::SkipToInitialBlock (common/log_reader.cc:35-57): start at the
+  // block holding initial_offset_, or the next one when that offset falls in
+  // a block's last 6 bytes (a trailer).  The reference calls it again on
+  // every ReadRecord until a record at or past the offset is returned, which
+  // only ever happens after the end of the file: the buffer is then empty,
+  // eof_ is set and the next read returns kEof again.
+  void SkipToInitialBlock() {
+    const uint64_t in_block = initial_offset_ % kBlockSize;
+    uint64_t block_start = initial_offset_ - in_block;
+    if (in_block > (uint64_t)kBlockSize - 6) block_start += kBlockSize;
+    if (skipped_) {  // the file is at its end (see above)
+      buf_begin_ = buf_end_ = block_start;
+      pos_ = size_;
+      return;
+    }
+    skipped_ = true;
+    buf_begin_ = buf_end_ = block_start;       // end_of_buffer_offset_ = block_start_location
+    pos_ = block_start < size_ ? block_start : size_;  // file_->Skip(block_start_location)
+  }
+
+  // log::Reader::ReadPhysicalRecord (common/log_reader.cc:179-256); reads
+  // come in kBlockSize pieces from the file position pos_.
   unsigned int ReadPhysicalRecord(size_t* frag, size_t* frag_len) {
     while (true) {
       const size_t avail = buf_end_ - buf_begin_;
       if (avail < (size_t)kHeaderSize) {
         if (!eof_) {  // the rest of this block is a trailer: read the next one
-          const size_t got = size_ - buf_end_ < (size_t)kBlockSize ? size_ - buf_end_
-                                                                    : (size_t)kBlockSize;
-          buf_begin_ = buf_end_;
-          buf_end_ += got;
+          const size_t got = size_ - pos_ < (size_t)kBlockSize ? size_ - pos_ : (size_t)kBlockSize;
+          buf_begin_ = pos_;   // (offsets equal file positions: the skip above keeps them so)
+          buf_end_ = pos_ + got;
+          pos_ += got;
           if (got < (size_t)kBlockSize) eof_ = true;
           continue;
         }
@@ -184,6 +209,11 @@ class Walk {
       *frag = buf_begin_ + kHeaderSize;
       *frag_len = length;
       buf_begin_ += kHeaderSize + length;
+      // a physical record that started before initial_offset_ is skipped
+      if (buf_begin_ - kHeaderSize - length < initial_offset_) {
+        *frag_len = 0;
+        return kBadRecord;
+      }
       return type;
     }
   }
@@ -198,8 +228,11 @@ class Walk {
     return next_ < checked_->size() && (*checked_)[next_] == header && (*ok_)[next_] != 0;
   }
 
+  // log::Reader::ReportDrop (common/log_reader.cc:171-176): drops that begin
+  // before initial_offset_ are not reported (uint64 arithmetic, as there).
   void Report(size_t bytes, const char* reason) {
-    if (reporter_ && !collect_) reporter_->Corruption(bytes, Status::Corruption(reason));
+    if (reporter_ && !collect_ && buf_begin_ - (uint64_t)bytes >= initial_offset_)
+      reporter_->Corruption(bytes, Status::Corruption(reason));
   }
 
   const uint8_t* file_;
@@ -209,8 +242,10 @@ class Walk {
   const std::vector<uint64_t>* checked_;
   const std::vector<uint8_t>* ok_;
   size_t next_ = 0;
-  uint64_t buf_begin_ = 0, buf_end_ = 0;
-  bool eof_ = false;
+  uint64_t initial_offset_;
+  uint64_t buf_begin_ = 0, buf_end_ = 0, pos_ = 0;
+  uint64_t last_record_offset_ = 0;
+  bool eof_ = false, skipped_ = false;
   std::string scratch_;
 };
 
@@ -270,8 +305,9 @@ Status BatchWriter::Seal(int device) {
   return Status::OK();
 }
 
-BatchReader::BatchReader(const char* file, size_t n, Reporter* reporter)
-    : file_(file), size_(n), reporter_(reporter), walk_(nullptr), last_record_offset_(0) {}
+BatchReader::BatchReader(const char* file, size_t n, Reporter* reporter, uint64_t initial_offset)
+    : file_(file), size_(n), reporter_(reporter), initial_offset_(initial_offset), walk_(nullptr),
+      last_record_offset_(0) {}
 
 BatchReader::~BatchReader() { delete walk_; }
 
@@ -281,7 +317,7 @@ Status BatchReader::Verify(int device) {
   walk_ = nullptr;
   headers_.clear();
   {  // pass 1: every header the reader could check (all checksums assumed good)
-    Walk collect(img, size_, nullptr, &headers_, nullptr, nullptr);
+    Walk collect(img, size_, initial_offset_, nullptr, &headers_, nullptr, nullptr);
     std::string rec;
     uint64_t off = 0;
     while (collect.ReadRecord(&rec, &off)) {
@@ -299,7 +335,7 @@ Status BatchReader::Verify(int device) {
     if (e != hipSuccess) return hip_status(e, "verify");
   }
   // pass 2 (ReadRecord): the reader itself, with the GPU's verdicts
-  walk_ = new Walk(img, size_, reporter_, nullptr, &headers_, &ok_);
+  walk_ = new Walk(img, size_, initial_offset_, reporter_, nullptr, &headers_, &ok_);
   return Status::OK();
 }
 
@@ -309,10 +345,11 @@ bool BatchReader::ReadRecord(std::string* record) {
 }
 
 Status ReadLog(int device, const char* file, size_t n, Reporter* reporter,
-               std::vector<std::string>* records, std::vector<uint64_t>* offsets) {
+               std::vector<std::string>* records, std::vector<uint64_t>* offsets,
+               uint64_t initial_offset) {
   if (records) records->clear();
   if (offsets) offsets->clear();
-  BatchReader reader(file, n, reporter);
+  BatchReader reader(file, n, reporter, initial_offset);
   Status s = reader.Verify(device);
   if (!s.ok()) return s;
   std::string rec;

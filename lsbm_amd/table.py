@@ -91,6 +91,22 @@ def seal_blocks(file_image, handles, types, stream=None, nbad=None):
     return nbad
 
 
+def trailer_crcs(file_image, handles, types, stream=None, out=None, nbad=None):
+    """Batched WriteRawBlock CRCs without touching the image: returns (masked
+    int32[n], nbad int32[1]); masked[i] is the trailer's crc field
+    Mask(Extend(Value(block i), &types[i], 1)), 0 for handles past the image."""
+    torch = _torch()
+    n = _check_image(file_image, handles, types)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=file_image.device)
+    if nbad is None:
+        nbad = torch.zeros(1, dtype=torch.int32, device=file_image.device)
+    check(lib().lsbm_sst_trailer_crcs_dev(_ptr(file_image), file_image.numel(), _ptr(handles),
+                                          _ptr(types), n, _ptr(out), _ptr(nbad),
+                                          _stream_ptr(stream)), "lsbm_sst_trailer_crcs_dev")
+    return out, nbad
+
+
 def verify_blocks(file_image, handles, stream=None):
     """Batched ReadBlock verify: returns (ok uint8[n], nbad int32[1]).  A
     handle past the image (truncated block read) is not ok."""

@@ -82,12 +82,13 @@ size_t ref_log_write(const char* payload, const uint64_t* offs, size_t n, char* 
   return out_copy(sink.data, out, cap);
 }
 
-// log::Reader(file, reporter, checksum=true, initial_offset=0) over image[0, n):
+// log::Reader(file, reporter, checksum=true, initial_offset) over image[0, n):
 // every ReadRecord result and Reporter call, in order, as event text.
-size_t ref_log_read(const char* image, size_t n, char* out, size_t cap) {
+size_t ref_log_read_from(const char* image, size_t n, uint64_t initial_offset, char* out,
+                         size_t cap) {
   StringSource src(image, n);
   Events ev;
-  leveldb::log::Reader r(&src, &ev, true, 0);
+  leveldb::log::Reader r(&src, &ev, true, initial_offset);
   leveldb::Slice rec;
   std::string scratch;
   while (r.ReadRecord(&rec, &scratch)) {
@@ -98,6 +99,10 @@ size_t ref_log_read(const char* image, size_t n, char* out, size_t cap) {
     ev.text += buf;
   }
   return out_copy(ev.text, out, cap);
+}
+
+size_t ref_log_read(const char* image, size_t n, char* out, size_t cap) {
+  return ref_log_read_from(image, n, 0, out, cap);
 }
 
 uint32_t ref_log_value(const char* p, size_t n) { return leveldb::crc32c::Value(p, n); }

@@ -80,10 +80,11 @@ int main(int argc, char** argv) {
     for (uint64_t h : w.headers()) printf("%llu\n", (unsigned long long)h);
     return 0;
   }
-  if (argc == 3 && !strcmp(argv[1], "read")) {
+  if ((argc == 3 || argc == 4) && !strcmp(argv[1], "read")) {
     const std::string img = slurp(argv[2]);
+    const uint64_t initial_offset = argc == 4 ? strtoull(argv[3], nullptr, 10) : 0;
     PrintReporter rep;  // prints each drop as it happens, between the records
-    lsbm::log::BatchReader reader(img.data(), img.size(), &rep);
+    lsbm::log::BatchReader reader(img.data(), img.size(), &rep, initial_offset);
     lsbm::Status s = reader.Verify(0);
     if (!s.ok()) {
       fprintf(stderr, "%s\n", s.ToString().c_str());
@@ -96,6 +97,6 @@ int main(int argc, char** argv) {
              (unsigned long long)reader.LastRecordOffset());
     return 0;
   }
-  fprintf(stderr, "usage: log_tool layout|write <payload> <offs> <out> [batch] | read <image>\n");
+  fprintf(stderr, "usage: log_tool layout|write <payload> <offs> <out> [batch] | read <image> [initial_offset]\n");
   return 2;
 }

@@ -86,6 +86,8 @@ def main():
     ref.ref_log_write.argtypes = [vp, vp, sz, vp, sz]
     ref.ref_log_read.restype = sz
     ref.ref_log_read.argtypes = [vp, sz, vp, sz]
+    ref.ref_log_read_from.restype = sz
+    ref.ref_log_read_from.argtypes = [vp, sz, ctypes.c_uint64, vp, sz]
     ref.ref_log_value.restype = ctypes.c_uint32
     ref.ref_log_value.argtypes = [vp, sz]
 
@@ -108,6 +110,12 @@ def main():
         b = np.ascontiguousarray(img, dtype=np.uint8)
         o = ctypes.create_string_buffer(1 << 22)
         k = ref.ref_log_read(b.ctypes.data, b.size, o, 1 << 22)
+        return o.raw[:k].decode()
+
+    def read_from(img, off):
+        b = np.ascontiguousarray(img, dtype=np.uint8)
+        o = ctypes.create_string_buffer(1 << 22)
+        k = ref.ref_log_read_from(b.ctypes.data, b.size, off, o, 1 << 22)
         return o.raw[:k].decode()
 
     def apply(img, ops):
@@ -173,6 +181,29 @@ def main():
     scenarios = []
     for name, ops in scen:
         scenarios.append({"name": name, "ops": ops, "events": read(apply(image, ops))})
+    # log::Reader with initial_offset != 0 (SkipToInitialBlock, the skip of
+    # physical records that start before the offset, unreported drops before
+    # it: common/log_reader.cc:35-57, 171-176, 247-251)
+    last = by_type[4][0]
+    offs_cases = [
+        ("at_zero", [], 0), ("one", [], 1), ("at_full_header", [], by_type[1][5]),
+        ("inside_full", [], by_type[1][5] + 9), ("at_first", [], first),
+        ("inside_first", [], first + 30), ("inside_middle", [], middle + 500),
+        ("inside_last", [], last + 11), ("block_1", [], BLOCK), ("block_1_minus_6", [], BLOCK - 6),
+        ("block_1_minus_5", [], BLOCK - 5), ("block_1_minus_1", [], BLOCK - 1),
+        ("block_2_plus_100", [], 2 * BLOCK + 100), ("near_end", [], n - 3), ("at_end", [], n),
+        ("past_end", [], n + 5000), ("far_past_end", [], n + 10 * BLOCK),
+        ("flip_before_offset_block", [["xor", full0 + HEADER + 3, 0x10]], BLOCK * (full0 // BLOCK + 1)),
+        ("flip_before_offset_same_block", [["xor", by_type[1][6] + HEADER + 1, 0x10]],
+         by_type[1][6] + 40),
+        ("flip_after_offset", [["xor", by_type[1][20] + HEADER + 2, 0x01]], by_type[1][19]),
+        ("truncated_after_offset", [["truncate", tail_heads[-1] + 3]], tail_heads[0]),
+    ]
+    offset_scenarios = []
+    for name, ops, off in offs_cases:
+        offset_scenarios.append({"name": name, "ops": ops, "initial_offset": int(off),
+                                 "events": read_from(apply(image, ops), int(off))})
+    assert offset_scenarios[0]["events"] == scenarios[0]["events"]
     fixture = {
         "source": "lsbm common/log_writer.cc + common/log_reader.cc built from /root/reference "
                   "(oracle/Makefile reflog); tests/golden/make_log_fixture.py",
@@ -180,13 +211,15 @@ def main():
         "image": {"bytes": int(n), "crc32c": value(image),
                   "header_crcs": [image[h:h + 4].tobytes().hex() for h in heads]},
         "scenarios": scenarios,
+        "offset_scenarios": offset_scenarios,
     }
     with open(os.path.join(HERE, "log_fixture.json"), "w") as f:
         json.dump(fixture, f, indent=0)
     kinds = sorted({line.split(" ", 2)[2] if line.startswith("D") else "R"
                     for s in scenarios for line in s["events"].splitlines()})
     print(f"{len(lens)} records, {len(heads)} physical, image {n} B, "
-          f"{len(scenarios)} scenarios; event kinds: {kinds}")
+          f"{len(scenarios)} scenarios, {len(offset_scenarios)} initial-offset scenarios; "
+          f"event kinds: {kinds}")
 
 
 if __name__ == "__main__":

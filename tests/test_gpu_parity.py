@@ -450,6 +450,12 @@ def test_sst_1M_x_4118_seal_verify_roundtrip(torch_cuda, oracle):
         assert int.from_bytes(img[off + L + 1:off + L + 5].tobytes(), "little") == oracle.mask(crc), i
     ok, nb = table.verify_blocks(d, dh)
     assert int(nb.item()) == 0 and bool(ok.all())
+    # the dense variant returns exactly the crc fields the seal wrote
+    tc, nb = table.trailer_crcs(d, dh, _dev(torch, types))
+    ends = handles[0::2] + L
+    stored = (img[ends + 1].astype(np.uint32) | (img[ends + 2].astype(np.uint32) << 8) |
+              (img[ends + 3].astype(np.uint32) << 16) | (img[ends + 4].astype(np.uint32) << 24))
+    assert int(nb.item()) == 0 and np.array_equal(_u32(tc), stored)
     bad = rng.choice(n, 30, replace=False)
     for j, i in enumerate(bad):
         off = int(handles[2 * i])
@@ -503,3 +509,44 @@ def test_sst_handles_past_the_image(torch_cuda, oracle):
     ok, nb = table.verify_blocks(d, dh)
     assert int(nb.item()) == len(bad)
     assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(bad)
+    tc, nb = table.trailer_crcs(d, dh, _dev(torch, types))
+    tch = _u32(tc)
+    assert int(nb.item()) == len(bad)
+    for i in range(sizes.size):
+        if i in bad:
+            assert tch[i] == 0
+        else:
+            off, sz = int(handles[2 * i]), int(sizes[i])
+            assert tch[i] == int.from_bytes(out[off + sz + 1:off + sz + 5].tobytes(), "little")
+
+
+@pytest.mark.parametrize("seed,smax", [(31, 130), (32, 70), (33, 5000)])
+def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax):
+    """Every trailer of a table whose blocks are 0..smax bytes: the seal writes
+    whole 64-B lines only where no other trailer shares them, bytes otherwise;
+    all trailers and every byte between them must come out exactly right."""
+    torch = torch_cuda
+    from lsbm_amd import table
+    rng = np.random.default_rng(seed)
+    n = 20000
+    sizes = rng.integers(0, smax, size=n)
+    sizes[rng.random(n) < 0.1] = 4118
+    handles, total = table.layout_blocks(sizes)
+    img = stream_bytes(seed, 0, total + 256)
+    types = rng.integers(0, 2, size=n).astype(np.uint8)
+    d = _dev(torch, img)
+    dh = _dev(torch, handles.astype(np.int64))
+    nbad = table.seal_blocks(d[:total], dh, _dev(torch, types))
+    assert int(nbad.item()) == 0
+    out = d.cpu().numpy()
+    want = img.copy()
+    ext = np.stack([handles[0::2], handles[1::2]], 1).astype(np.uint64).reshape(-1)
+    offs = np.empty(n + 1, dtype=np.uint64)
+    for i in range(n):
+        off, sz = int(handles[2 * i]), int(sizes[i])
+        crc = oracle.mask(oracle.extend(oracle.value(img[off:off + sz].tobytes()), bytes([types[i]])))
+        want[off + sz] = types[i]
+        want[off + sz + 1:off + sz + 5] = np.frombuffer(int(crc).to_bytes(4, "little"), np.uint8)
+    assert np.array_equal(out, want)
+    ok, nb = table.verify_blocks(d[:total], dh)
+    assert int(nb.item()) == 0 and bool(ok.all())

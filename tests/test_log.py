@@ -163,6 +163,32 @@ def test_batch_reader_matches_reference_reader(torch_cuda, fx, log_tool, tmp_pat
 
 
 @pytest.mark.gpu
+def test_batch_reader_initial_offset_matches_reference_reader(torch_cuda, fx, log_tool, tmp_path):
+    """BatchReader with initial_offset != 0: SkipToInitialBlock, records that
+    start before the offset skipped, drops before it unreported -- the same
+    events as the reference's log::Reader (common/log_reader.cc:35-57,
+    171-176, 247-251) on every initial-offset scenario of the fixture."""
+    d, payload, offs = fx
+    p, o = _files(tmp_path, payload, offs)
+    out = tmp_path / "layout.bin"
+    r = subprocess.run([log_tool, "layout", p, o, str(out)], capture_output=True, text=True,
+                       check=True)
+    heads = [int(x) for x in r.stdout.split()]
+    base = _reference_image(d, np.fromfile(out, dtype=np.uint8), heads)
+    assert len(d["offset_scenarios"]) >= 20
+    failed = []
+    for s in d["offset_scenarios"]:
+        img = _apply(base, s["ops"])
+        path = tmp_path / f"off_{s['name']}.bin"
+        img.tofile(path)
+        got = subprocess.run([log_tool, "read", str(path), str(s["initial_offset"])],
+                             capture_output=True, text=True, check=True, timeout=120).stdout
+        if got != s["events"]:
+            failed.append(s["name"])
+    assert not failed, failed
+
+
+@pytest.mark.gpu
 def test_log_seal_and_verify_entry_points(torch_cuda, oracle):
     """lsbm_log_seal_dev / lsbm_log_verify_dev on a framed image: seals equal
     Mask(Extend(type_crc_[t], payload)) (common/log_writer.cc:86-87), verify

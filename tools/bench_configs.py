@@ -49,8 +49,15 @@ def zipf_lengths(n, seed=0x5EED0002, ranks=128, theta=0.99):
     return np.minimum(65536, 512 * r + u).astype(np.int64)
 
 
-def time_launches(fn, stream, reps=10, warm=2):
+def time_launches(fn, stream, reps=10, warm=2, spin_s=0.3):
+    """Seconds per launch of fn.  Before the warm-up launches, fn runs for
+    spin_s seconds: after host-side pauses the GPU clock has dropped, and a
+    few launches are not enough to bring it back."""
     import torch
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < spin_s:
+        fn()
+        torch.cuda.synchronize()
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -87,6 +94,28 @@ def config3(args):
                       "GiBps": round(n * L / t / 2**30, 1), "GBps": round(gbps, 1),
                       "pct_hbm_peak": round(100 * gbps / HBM, 2), "sample_mismatches": bad}),
           flush=True)
+    del d
+
+
+def units4k(args):
+    """config 2's geometry (1M x 4096 B, stride 4096) through the ragged
+    kernel (offsets batch): the ragged path's overhead against the fixed one."""
+    import torch
+    from lsbm_amd import engine
+    n, L, seed = 1 << 20, 4096, 0x5EED0000
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, seed)
+    offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device="cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    t = time_launches(lambda: engine.crc32c_batch(d, offs, out=out, stream=s), s)
+    ref = engine.crc32c_fixed(d, L, L, n)
+    tf = time_launches(lambda: engine.crc32c_fixed(d, L, L, n, out=ref, stream=s), s)
+    gbps, gf = n * L / t / 1e9, n * L / tf / 1e9
+    print(json.dumps({"config": "units4k", "blocks": n, "ms": round(t * 1e3, 3), "GBps": round(gbps, 1),
+                      "pct_hbm_peak": round(100 * gbps / HBM, 2),
+                      "fixed_pct_hbm_peak": round(100 * gf / HBM, 2),
+                      "agree_with_fixed": bool(torch.equal(out, ref))}), flush=True)
     del d
 
 
@@ -177,12 +206,28 @@ def sst4118(args):
     types = torch.zeros(n, dtype=torch.uint8, device="cuda")
     t_seal = time_launches(lambda: table.seal_blocks(d, handles, types, stream=s), s, reps=10)
     t_ver = time_launches(lambda: table.verify_blocks(d, handles, stream=s), s, reps=10)
+    tc_out = torch.empty(n, dtype=torch.int32, device="cuda")
+    tc_nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    t_tc = time_launches(lambda: table.trailer_crcs(d, handles, types, stream=s, out=tc_out,
+                                                    nbad=tc_nbad), s, reps=10)
+    img = d.cpu().numpy()
+    tc_host = tc_out.cpu().numpy().view(np.uint32)
+    ends = offs[:-1] + L
+    stored = (img[ends + 1].astype(np.uint32) | (img[ends + 2].astype(np.uint32) << 8) |
+              (img[ends + 3].astype(np.uint32) << 16) | (img[ends + 4].astype(np.uint32) << 24))
+    g_tc = n * L / t_tc / 1e9
+    # the extents timing again, after the others (clock / ordering check)
+    t2 = time_launches(lambda: engine.crc32c_extents(d, de, out=out, stream=s), s, reps=10)
     ok, nbad = table.verify_blocks(d, handles, stream=s)
     g_seal, g_ver = n * (L + 1) / t_seal / 1e9, n * (L + 1) / t_ver / 1e9
     print(json.dumps({"config": "sst4118", "blocks": n, "block_bytes": L + 1, "ms": round(t * 1e3, 3),
                       "GBps": round(gbps, 1), "pct_hbm_peak": round(100 * gbps / HBM, 2),
                       "sst_seal": {"ms": round(t_seal * 1e3, 3), "GBps": round(g_seal, 1),
                                    "pct_hbm_peak": round(100 * g_seal / HBM, 2)},
+                      "ext_again_pct_hbm_peak": round(100 * n * (L + 1) / t2 / 1e9 / HBM, 2),
+                      "sst_trailer_crcs": {"ms": round(t_tc * 1e3, 3), "GBps": round(g_tc, 1),
+                                           "pct_hbm_peak": round(100 * g_tc / HBM, 2),
+                                           "equal_sealed": bool(np.array_equal(tc_host, stored))},
                       "sst_verify": {"ms": round(t_ver * 1e3, 3), "GBps": round(g_ver, 1),
                                      "pct_hbm_peak": round(100 * g_ver / HBM, 2),
                                      "all_ok": bool(ok.all()) and int(nbad.item()) == 0},
@@ -268,7 +313,7 @@ def main():
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"sst4118": sst4118, "config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
+        {"sst4118": sst4118, "units4k": units4k, "config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
 
 
 if __name__ == "__main__":
