@@ -297,6 +297,16 @@ __device__ __forceinline__ void extent_from_raw(const RaggedArgs& a, uint64_t b,
   }
 }
 
+// a / b for b >= 1: float reciprocal and one correction each way (exact for
+// a < 2^24, i.e. blocks under 2 GiB); the integer divide beyond that.
+__device__ __forceinline__ uint32_t div_u32(uint32_t a, uint32_t b) {
+  if (a >= (1u << 24)) return a / b;
+  uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
+  const int32_t r = (int32_t)(a - q * b);
+  q = r < 0 ? q - 1u : ((uint32_t)r >= b ? q + 1u : q);
+  return q;
+}
+
 struct Frame {
   uint64_t s, e, row0, rows;  // rows >= 1
   uint32_t units;             // ceil(rows / max_rows)
@@ -310,10 +320,11 @@ __device__ __forceinline__ Frame frame_of(uint64_t s, uint64_t e, uint32_t max_r
   f.row0 = (s - 4) >> 7;
   const uint64_t row_end = (e + 127) >> 7;
   f.rows = row_end > f.row0 ? row_end - f.row0 : 1;
-  f.units = (uint32_t)((f.rows + max_rows - 1) / max_rows);
-  // rows < 2^32 (blocks under 512 GiB): 32-bit division
-  f.q = (uint32_t)f.rows / f.units;
-  f.rem = (uint32_t)f.rows - f.q * f.units;
+  // rows < 2^32 (blocks under 512 GiB): 32-bit unit arithmetic
+  const uint32_t r32 = (uint32_t)f.rows;
+  f.units = (r32 + max_rows - 1) / max_rows;  // constant divisor: multiply-high
+  f.q = f.units == 1u ? r32 : div_u32(r32, f.units);
+  f.rem = r32 - f.q * f.units;
   return f;
 }
 
@@ -413,38 +424,40 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
 
   // The block still open at the end of the last retired round and the xor of
   // its units so far (wave-uniform); ~0 = none.
-  uint64_t carry_b = ~0ull;
+  uint32_t carry_b = ~0u;  // block index relative to b_lo
   uint32_t carry_v = 0;
   // the previous round: braids, unit and block, and what its finish needs
   uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
   u32x4 pshift = {0, 0, 0, 0}, pfin = {0, 0, 0, 0};
   uint32_t paux0 = 0, paux1 = 0;
   uint64_t pk = 0, pb = 0, pat = 0;
-  bool pact = false, plast = false, pfits = true;
+  bool pact = false, plast = false, pfits = true, pfast = false;
 
   uint64_t pend_a = 0;  // this lane's parked result (0 = none), see retire()
   uint32_t pend_v = 0, pend_i = 0;
   uint32_t round = 0;   // rounds retired so far (wave-uniform)
   auto retire = [&]() {
     const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
-    uint32_t v = cols_apply(pshift, raw, li);        // A^(128 (k mod 512))
-    if (pk >= kShiftCols) v = shift_rows(g_lds, dc, v, pk & ~(uint64_t)(kShiftCols - 1));
-    v = pact ? v : 0u;
-    const uint64_t key = pact ? pb : ~0ull;
-    // segmented inclusive xor-scan over the 8 groups (blocks non-decreasing in g)
+    uint32_t v = raw;
+    if (!pfast) {  // (a fast round: 8 whole blocks, no shift, no sum, no carry)
+      v = cols_apply(pshift, raw, li);  // A^(128 (k mod 512))
+      if (pk >= kShiftCols) v = shift_rows(g_lds, dc, v, pk & ~(uint64_t)(kShiftCols - 1));
+      v = pact ? v : 0u;
+      const uint32_t key = pact ? (uint32_t)(pb - b_lo) : ~0u;  // a range is < 2^32 blocks
+      // segmented inclusive xor-scan over the 8 groups (blocks non-decreasing in g)
 #pragma unroll
-    for (uint32_t d = 8; d < 64; d <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)v, d);
-      const uint64_t tk = (uint64_t)__shfl_up((unsigned long long)key, d);
-      if (lane >= d && tk == key) v ^= t;
+      for (uint32_t d = 8; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, d);
+        const uint32_t tk = (uint32_t)__shfl_up((int)key, d);
+        if (lane >= d && tk == key) v ^= t;
+      }
+      if (pact && key == carry_b) v ^= carry_v;
+      // the block open after group 7 carries into the next round
+      const uint32_t key7 = __builtin_amdgcn_readlane(key, 56);
+      const uint32_t last7 = __builtin_amdgcn_readlane((uint32_t)plast, 56);
+      carry_v = __builtin_amdgcn_readlane(v, 56);
+      carry_b = (key7 != ~0u && !last7) ? key7 : ~0u;
     }
-    if (pact && key == carry_b) v ^= carry_v;
-    // the block open after group 7 carries into the next round
-    const uint64_t key7 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), 56) << 32) |
-                          __builtin_amdgcn_readlane((uint32_t)key, 56);
-    const uint32_t last7 = __builtin_amdgcn_readlane((uint32_t)plast, 56);
-    carry_v = __builtin_amdgcn_readlane(v, 56);
-    carry_b = (key7 != ~0ull && !last7) ? key7 : ~0ull;
     // finish: register after the block = A^-z(v) (A^(1-z) for the seal's type byte)
     const uint32_t l = cols_apply(pfin, v, li);
     const uint32_t crc = l ^ 0xffffffffu;
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       // scattered writes cost ~13% of HBM peak (A/B: the same 4-byte writes
       // added to verify took it from 75% to 62%; whole 64-B line writes were
       // no better): lsbm_sst_trailer_crcs_dev returns dense CRCs instead.
-      if (li < kTrailer)
+      if (li < kTrailer)  // (non-temporal stores: no different, A/B)
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(li == 0 ? typ : m >> (8 * (li - 1)));
     } else if constexpr (mode == kModeSstCrc) {  // the same crc, dense: out[b]
       const uint32_t typ = paux0 & 0xffu;
@@ -501,19 +514,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       if (pfits && li < 4)
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(unaligned_word(paux0, paux1, pat) >> (8 * li));
 #endif
-#ifdef LSBM_DIAG_VERIFY_WRITEBACK_DW  // diagnostic builds only: rewrite the covering dwords
-      if (pfits && li == 0) {
-        reinterpret_cast<uint32_t*>(pat & ~3ull)[0] = paux0;
-        reinterpret_cast<uint32_t*>((pat + 3) & ~3ull)[0] = paux1;
-      }
-#endif
-#ifdef LSBM_DIAG_VERIFY_WRITEBACK_64  // diagnostic builds only: rewrite the covering 64-B line
-      if (pfits && li < 4) {
-        u32x4* q = reinterpret_cast<u32x4*>((pat & ~63ull) + 16 * li);
-        const u32x4 v = *q;
-        *q = v;
-      }
-#endif
       if (mine) {
         pend_a = reinterpret_cast<uint64_t>(args.ok + pb);
         pend_v = good ? 1u : 0u;
@@ -539,11 +539,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
         h[3] = (uint8_t)(pend_v >> 24);
         if (args.out) args.out[b_lo + pend_i] = pend_v;
       } else if constexpr (mode == kModeOut || mode == kModeSstCrc) {
-#ifdef LSBM_DIAG_OUT_BYTE  // diagnostic builds only: one byte per block instead of a dword
-        reinterpret_cast<uint8_t*>(args.out)[(pend_a - reinterpret_cast<uint64_t>(args.out)) / 4] = (uint8_t)pend_v;
-#else
         *reinterpret_cast<uint32_t*>(pend_a) = pend_v;
-#endif
       } else {
         *reinterpret_cast<uint8_t*>(pend_a) = (uint8_t)pend_v;
       }
@@ -563,26 +559,36 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const Frame ft = frame_of(sj, ej, kMaxRows);
     const bool vj = lane < 9u && cur_b + lane < b_hi;
     const uint32_t units_j = vj ? ft.units : 0u;
-    uint32_t pre = units_j;
+    // Fast round: the cursor is at a block start and the next 8 blocks are
+    // one unit each, so group g takes block cur_b + g (every round over an
+    // SSTable's data blocks).  Wave-uniform.
+    const bool fast = cur_o == 0u && __ballot(lane < 8u && units_j == 1u) == 0xffull;
+    uint32_t jg = g, jnext = 8, pre_before = g, pre8 = 8;
+    if (!fast) {
+      uint32_t pre = units_j;
 #pragma unroll
-    for (uint32_t d = 1; d < 16; d <<= 1) {  // lanes >= 9 contribute 0: a 16-lane scan suffices
-      const uint32_t t = (uint32_t)__shfl_up((int)pre, d, 16);
-      if ((lane & 15u) >= d) pre += t;
+      for (uint32_t d = 1; d < 16; d <<= 1) {  // lanes >= 9 contribute 0: a 16-lane scan suffices
+        const uint32_t t = (uint32_t)__shfl_up((int)pre, d, 16);
+        if ((lane & 15u) >= d) pre += t;
+      }
+      jg = 0;
+      jnext = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 9; q++) {
+        // count of lanes (among the first 9) whose prefix <= cur_o + q
+        const uint64_t m = __ballot((lane < 9) && pre <= cur_o + q);
+        const uint32_t c = (uint32_t)__builtin_popcountll(m);
+        if (q == g) jg = c;
+        if (q == 8) jnext = c;
+      }
+      // shuffles run with every lane active (a bpermute from an inactive
+      // source lane reads 0), then select
+      const uint32_t pre_prev = (uint32_t)__shfl((int)pre, (int)(jg ? jg - 1 : 0));
+      pre_before = jg ? pre_prev : 0u;
+      const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
+      pre8 = jnext ? pre8_prev : 0u;
     }
     const uint32_t my_t = cur_o + g;  // this group's unit, as an offset from the cursor
-    uint32_t jg = 0, jnext = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 9; q++) {
-      // count of lanes (among the first 9) whose prefix <= cur_o + q
-      const uint64_t m = __ballot((lane < 9) && pre <= cur_o + q);
-      const uint32_t c = (uint32_t)__builtin_popcountll(m);
-      if (q == g) jg = c;
-      if (q == 8) jnext = c;
-    }
-    // shuffles run with every lane active (a bpermute from an inactive
-    // source lane reads 0), then select
-    const uint32_t pre_prev = (uint32_t)__shfl((int)pre, (int)(jg ? jg - 1 : 0));
-    const uint32_t pre_before = jg ? pre_prev : 0u;
     const uint64_t b = cur_b + jg;
     const bool active = jg < 9 && b < b_hi;
     Frame f = {0, 0, 0, 1, 1, 1, 0};
@@ -598,8 +604,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint64_t at = __shfl((unsigned long long)atj, (int)jg);
     const uint32_t o = my_t - pre_before;
     // the cursor after these 8 units, and the next round's extents
-    const uint32_t pre8_prev = (uint32_t)__shfl((int)pre, (int)(jnext ? jnext - 1 : 0));
-    const uint32_t pre8 = jnext ? pre8_prev : 0u;
     const uint64_t nb = cur_b + jnext;
     const uint32_t no = cur_o + 8 - pre8;
     ExtRaw rn;
@@ -720,11 +724,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       // the (r < rows) branch, the vmcnt wait sat on that path alone, and the
       // next reload of the bank had to drain every load still in flight.
       asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
-#ifdef LSBM_DIAG_NOGUARD  // diagnostic builds only (wrong CRCs): every row absorbed
-      STEP_ROW(w);
-#else
       if (r < rows) STEP_ROW(w);
-#endif
     };
     // The start fix (init bytes, bytes before s) only ever falls on rows 0
     // and 1 of a unit: chunk c of row 0 has c <= s - 4 and the fix chunk has
@@ -781,6 +781,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     p1 = c1;
     p2 = c2;
     p3 = c3;
+    pfast = fast;
     pact = (st_i >> 26) & 1u;
     plast = (st_i >> 24) & 1u;
     pfits = (st_i >> 25) & 1u;

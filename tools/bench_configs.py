@@ -49,11 +49,13 @@ def zipf_lengths(n, seed=0x5EED0002, ranks=128, theta=0.99):
     return np.minimum(65536, 512 * r + u).astype(np.int64)
 
 
-def time_launches(fn, stream, reps=10, warm=2, spin_s=0.3):
+def time_launches(fn, stream, reps=10, warm=2, spin_s=None):
     """Seconds per launch of fn.  Before the warm-up launches, fn runs for
     spin_s seconds: after host-side pauses the GPU clock has dropped, and a
     few launches are not enough to bring it back."""
     import torch
+    if spin_s is None:  # LSBM_SPIN_S=0 under rocprofv3 --pmc (every dispatch is counted)
+        spin_s = float(os.environ.get("LSBM_SPIN_S", "0.3"))
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < spin_s:
         fn()
@@ -117,6 +119,28 @@ def units4k(args):
                       "fixed_pct_hbm_peak": round(100 * gf / HBM, 2),
                       "agree_with_fixed": bool(torch.equal(out, ref))}), flush=True)
     del d
+
+
+def c4uniform(args):
+    """config 4's byte count with every block the same length (the mean, 12,534 B):
+    what config 4 would run at if the units of a round were equal (lockstep)."""
+    import torch
+    from lsbm_amd import engine
+    n = args.c4_blocks
+    lens = np.full(n, 12534, dtype=np.int64)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    offs += 5
+    d = torch.empty(int(offs[-1]) + 16, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 0x5EED0003)
+    do = torch.from_numpy(offs).to("cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    t = time_launches(lambda: engine.crc32c_batch(d, do, out=out, stream=s), s, reps=5, warm=1)
+    gbps = int(lens.sum()) / t / 1e9
+    print(json.dumps({"config": "c4uniform", "blocks": n, "ms": round(t * 1e3, 3),
+                      "pct_hbm_peak": round(100 * gbps / HBM, 2)}), flush=True)
+    del d, do
 
 
 def config4(args):
@@ -313,7 +337,7 @@ def main():
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"sst4118": sst4118, "units4k": units4k, "config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
+        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
 
 
 if __name__ == "__main__":
