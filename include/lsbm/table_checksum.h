@@ -39,7 +39,9 @@ static const size_t kBlockTrailerSize = 5;
 std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64_t* file_size);
 
 // Batched WriteRawBlock: for every handle, writes the trailer at
-// file[offset + size, offset + size + 5) with type = types[i].
+// file[offset + size, offset + size + 5) with type = types[i].  A handle
+// whose size + 5 bytes leave the image is Corruption("truncated block read")
+// (table/format.cc:88-91) and nothing is written.
 Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
                   const uint8_t* types, size_t n);
 
@@ -47,6 +49,26 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
 // Returns Corruption("block checksum mismatch") if any block fails.
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
                     size_t n, std::vector<uint8_t>* ok);
+
+// One table file image in host memory: its blocks and, for sealing, their
+// CompressionType bytes.
+struct TableImage {
+  char* file;
+  size_t file_size;
+  const BlockHandle* handles;
+  const uint8_t* types;  // SealTables only
+  size_t n;
+};
+
+// SealBlocks / VerifyBlocks over many tables at once (the output tables of a
+// compaction, lsbm/db_impl.cc:843-892): the blocks of all of them stream
+// through one pipeline (64 MiB chunks, three in flight: host copy, PCIe and
+// the kernel overlap), and only 4 B (seal) or 1 B (verify) per block comes
+// back from the device.  VerifyTables' ok holds the tables' flags one after
+// the other.  A page-locked image (hipHostMalloc / hipHostRegister) is DMA-ed
+// in place; a pageable one is copied into pinned staging first.
+Status SealTables(int device, const TableImage* tables, size_t count);
+Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok);
 
 }  // namespace lsbm
 

@@ -8,8 +8,9 @@
  * (`void* stream` is a hipStream_t; NULL = the legacy default stream); they
  * only enqueue work, never synchronise, and may be captured into a hipGraph
  * once the device has been initialised with lsbm_crc32c_init().
- * They are thread-safe: per-device tables are built once (std::call_once) and
- * are read-only afterwards; callers serialise through their own streams.
+ * They are thread-safe: per-device tables are built once (on first use) and
+ * are read-only until lsbm_crc32c_shutdown(); callers serialise through their
+ * own streams.
  *
  * Reference interfaces replaced (lsbm = tengdj/lsbm, a LevelDB 1.15 fork):
  *   util/crc32c.h:17-40      crc32c::Extend / Value / Mask / Unmask
@@ -61,6 +62,11 @@ uint32_t lsbm_crc32c_unmask(uint32_t masked_crc);
 /* Builds the per-device tables (idempotent, thread-safe).  Optional: every
  * _dev call initialises lazily, but graph capture needs it done beforehand. */
 int lsbm_crc32c_init(int device);
+/* Frees everything the library holds on every device: the tables, the
+ * host-staged batch slots and the C++ layers' staging (pinned and device
+ * buffers, streams).  Call it with no library work in flight or pending
+ * (it synchronises the devices it touches); the next call re-initialises. */
+int lsbm_crc32c_shutdown(void);
 /* Library version string and the last HIP error text seen on this thread. */
 const char* lsbm_crc32c_version(void);
 const char* lsbm_crc32c_last_error(void);
@@ -135,6 +141,10 @@ int lsbm_sst_verify_dev(const uint8_t* d_file, uint64_t file_bytes, const uint64
  * masked values.  Records that do not fit are left untouched (d_masked 0). */
 int lsbm_log_seal_dev(uint8_t* d_log, uint64_t log_bytes, const uint64_t* d_headers,
                       uint64_t n_records, uint32_t* d_masked, uint32_t* d_nbad, void* stream);
+/* The same masked CRCs into d_masked (required) without writing the image:
+ * for a host that frames the log itself (include/lsbm/log_checksum.h). */
+int lsbm_log_crcs_dev(const uint8_t* d_log, uint64_t log_bytes, const uint64_t* d_headers,
+                      uint64_t n_records, uint32_t* d_masked, uint32_t* d_nbad, void* stream);
 /* log::Reader::ReadPhysicalRecord's checksum (common/log_reader.cc:228-242):
  * d_ok[i] = 1 iff the record fits and
  * Unmask(DecodeFixed32(header)) == Value(header + 6, 1 + length). */
@@ -149,6 +159,13 @@ int lsbm_log_verify_dev(const uint8_t* d_log, uint64_t log_bytes, const uint64_t
 int lsbm_crc32c_batch_host(int device, const void* h_base, const uint64_t* h_offsets,
                            uint64_t n_blocks, const uint32_t* h_init, uint32_t* h_out,
                            uint32_t flags);
+
+/* ---- device helpers ----
+ * d_dst[d_dst_off[i], +d_len[i]) = d_src[d_src_off[i], +d_len[i]) for i < n
+ * (segments must not overlap each other's destinations): compacts
+ * variable-length results before a D2H copy. */
+int lsbm_gather_dev(const void* d_src, const uint64_t* d_src_off, const uint64_t* d_len, uint64_t n,
+                    void* d_dst, const uint64_t* d_dst_off, void* stream);
 
 /* ---- benchmark / diagnostic helpers (not on the checksum path) ---- */
 /* d_buf[k] = byte k of the splitmix64 stream `seed`. */

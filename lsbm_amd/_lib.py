@@ -33,6 +33,7 @@ SIGNATURES = {
     "lsbm_crc32c_mask": (_u32, [_u32]),
     "lsbm_crc32c_unmask": (_u32, [_u32]),
     "lsbm_crc32c_init": (_int, [_int]),
+    "lsbm_crc32c_shutdown": (_int, []),
     "lsbm_crc32c_version": (ctypes.c_char_p, []),
     "lsbm_crc32c_last_error": (ctypes.c_char_p, []),
     "lsbm_crc32c_fixed_dev": (_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u32, _vp]),
@@ -44,7 +45,9 @@ SIGNATURES = {
     "lsbm_sst_trailer_crcs_dev": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_log_seal_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_log_verify_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "lsbm_log_crcs_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_crc32c_batch_host": (_int, [_int, _vp, _vp, _u64, _vp, _vp, _u32]),
+    "lsbm_gather_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),
     "lsbm_stream_read_dev": (_int, [_vp, _u64, _vp, _vp]),
     # include/lsbm_bloom.h

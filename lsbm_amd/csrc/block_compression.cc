@@ -1,8 +1,10 @@
 // block_compression.cc -- include/lsbm/block_compression.h on top of the C
-// ABI (include/lsbm_snappy.h).  The blocks are staged to the device once,
-// (de)compressed there in one launch, and the results come back whole through
-// the pinned bounce; only WriteBlock's keep-or-not rule and the assembly of
-// the output run on the host.
+// ABI (include/lsbm_snappy.h).  The blocks go to the device once through the
+// device's HostSession (host_session.h: persistent streams and buffers, the
+// caller's current device restored after), are (de)compressed there in one
+// launch, and only the bytes the host keeps come back: compressed blocks are
+// compacted on the device first (lsbm_gather_dev), never their capacity slots.
+// WriteBlock's keep-or-not rule and the assembly of the output run on the host.
 #include "../../include/lsbm/block_compression.h"
 
 #include <hip/hip_runtime_api.h>
@@ -10,44 +12,16 @@
 
 #include "../../include/lsbm_crc32c.h"
 #include "../../include/lsbm_snappy.h"
-#include "host_stage.h"
+#include "host_session.h"
 
 namespace lsbm {
 
 namespace {
 
-// Device allocations of one call, freed after the call's stream drains.
-struct DeviceScratch {
-  std::vector<void*> ptrs;
-  PinnedBounce bounce;
-  CallStream stream;
-  hipError_t alloc(void** p, size_t bytes) {
-    const hipError_t e = hipMalloc(p, bytes ? bytes : 1);
-    if (e == hipSuccess) ptrs.push_back(*p);
-    return e;
-  }
-  ~DeviceScratch() {
-    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
-    for (void* p : ptrs) (void)hipFree(p);
-  }
-};
-
-Status hip_status(hipError_t e, const char* what) {
-  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
 Status check_offsets(const uint64_t* offsets, size_t n) {
   for (size_t i = 0; i < n; i++)
     if (offsets[i + 1] < offsets[i]) return Status::InvalidArgument("offsets must not decrease");
   return Status::OK();
-}
-
-// Makes `device` current; call before a DeviceScratch is made, so that its
-// stream belongs to that device.
-Status open_device(int device) {
-  if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
-  const hipError_t e = hipSetDevice(device);
-  return e == hipSuccess ? Status::OK() : hip_status(e, "device");
 }
 
 // Rebase offsets[0..n] to start at 0 (the staged copy starts at offsets[0]).
@@ -56,6 +30,11 @@ std::vector<uint64_t> rebased(const uint64_t* offsets, size_t n) {
   for (size_t i = 0; i <= n; i++) r[i] = offsets[i] - offsets[0];
   return r;
 }
+
+// The most a snappy stream of c bytes can expand to: its largest tag ratio
+// is a 3-byte copy emitting 64 bytes (21.3x).  A preamble claiming more
+// cannot be met, so RawUncompress fails it; it gets no output window.
+constexpr uint64_t kMaxExpansion = 22;
 
 }  // namespace
 
@@ -75,44 +54,61 @@ Status CompressBlocks(int device, const char* raw, const uint64_t* offsets, size
   std::vector<uint64_t> cap(n + 1, 0);  // output slots of MaxCompressedLength bytes
   for (size_t i = 0; i < n; i++) cap[i + 1] = cap[i] + lsbm_snappy_max_compressed_length(off[i + 1] - off[i]);
 
-  s = open_device(device);
+  SessionLease ss;
+  s = ss.Open(device);
   if (!s.ok()) return s;
-  DeviceScratch d;
-  if (d.stream.status() != hipSuccess) return hip_status(d.stream.status(), "stream");
-  const hipStream_t st = d.stream.get();
-  void *d_raw = nullptr, *d_off = nullptr, *d_cap = nullptr, *d_comp = nullptr, *d_len = nullptr;
-  hipError_t e = d.alloc(&d_raw, total);
-  if (e == hipSuccess) e = d.alloc(&d_off, (n + 1) * sizeof(uint64_t));
-  if (e == hipSuccess) e = d.alloc(&d_cap, (n + 1) * sizeof(uint64_t));
-  if (e == hipSuccess) e = d.alloc(&d_comp, cap[n]);
-  if (e == hipSuccess) e = d.alloc(&d_len, n * sizeof(uint64_t));
-  if (e == hipSuccess) e = d.bounce.to_device(d_raw, raw + offsets[0], total, st);
-  if (e == hipSuccess) e = d.bounce.to_device(d_off, off.data(), (n + 1) * sizeof(uint64_t), st);
-  if (e == hipSuccess) e = d.bounce.to_device(d_cap, cap.data(), (n + 1) * sizeof(uint64_t), st);
+  const hipStream_t st = ss->stream();
+  void *d_raw, *d_off, *d_cap, *d_comp, *d_len;
+  hipError_t e = ss->scratch(0, total, &d_raw);
+  if (e == hipSuccess) e = ss->scratch(1, (n + 1) * sizeof(uint64_t), &d_off);
+  if (e == hipSuccess) e = ss->scratch(2, (n + 1) * sizeof(uint64_t), &d_cap);
+  if (e == hipSuccess) e = ss->scratch(3, cap[n], &d_comp);
+  if (e == hipSuccess) e = ss->scratch(4, n * sizeof(uint64_t), &d_len);
+  if (e == hipSuccess) e = ss->upload(d_raw, raw + offsets[0], total);
+  if (e == hipSuccess) e = ss->upload(d_off, off.data(), (n + 1) * sizeof(uint64_t));
+  if (e == hipSuccess) e = ss->upload(d_cap, cap.data(), (n + 1) * sizeof(uint64_t));
   if (e != hipSuccess) return hip_status(e, "staging");
   if (lsbm_snappy_compress_dev(d_raw, static_cast<const uint64_t*>(d_off), n, static_cast<uint8_t*>(d_comp),
                                static_cast<const uint64_t*>(d_cap), static_cast<uint64_t*>(d_len),
                                st) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
   std::vector<uint64_t> clen(n);
-  std::string comp(cap[n], '\0');
-  e = d.bounce.to_host(clen.data(), d_len, n * sizeof(uint64_t), st);
-  if (e == hipSuccess) e = d.bounce.to_host(&comp[0], d_comp, cap[n], st);
+  e = ss->download(clen.data(), d_len, n * sizeof(uint64_t));
   if (e != hipSuccess) return hip_status(e, "compress");
 
-  // WriteBlock's rule (table/table_builder.cc:187-188), block by block
+  // WriteBlock's rule (table/table_builder.cc:187-188), block by block: only
+  // the blocks kept compressed have their bytes gathered and brought back
   types->resize(n);
+  std::vector<uint64_t> keep_len(n, 0), dense(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t len = off[i + 1] - off[i];
+    const bool keep = clen[i] != ~0ull && clen[i] < len - len / 8;
+    (*types)[i] = keep ? kSnappyCompression : kNoCompression;
+    keep_len[i] = keep ? clen[i] : 0;
+    dense[i + 1] = dense[i] + keep_len[i];
+  }
+  std::string comp(dense[n], '\0');
+  if (dense[n]) {
+    void *d_keep, *d_dense, *d_packed;
+    e = ss->scratch(4, n * sizeof(uint64_t), &d_keep);  // (d_len is no longer needed)
+    if (e == hipSuccess) e = ss->scratch(5, (n + 1) * sizeof(uint64_t), &d_dense);
+    if (e == hipSuccess) e = ss->scratch(6, dense[n], &d_packed);
+    if (e == hipSuccess) e = ss->upload(d_keep, keep_len.data(), n * sizeof(uint64_t));
+    if (e == hipSuccess) e = ss->upload(d_dense, dense.data(), (n + 1) * sizeof(uint64_t));
+    if (e != hipSuccess) return hip_status(e, "staging");
+    if (lsbm_gather_dev(d_comp, static_cast<const uint64_t*>(d_cap), static_cast<const uint64_t*>(d_keep), n,
+                        d_packed, static_cast<const uint64_t*>(d_dense), st) != LSBM_OK)
+      return Status::IOError(lsbm_crc32c_last_error());
+    e = ss->download(&comp[0], d_packed, dense[n]);
+    if (e != hipSuccess) return hip_status(e, "compress");
+  }
   out_offsets->resize(n + 1);
   out->reserve(total);
   for (size_t i = 0; i < n; i++) {
-    const uint64_t len = off[i + 1] - off[i];
-    if (clen[i] != ~0ull && clen[i] < len - len / 8) {
-      out->append(comp, cap[i], clen[i]);
-      (*types)[i] = kSnappyCompression;
-    } else {
-      out->append(raw + offsets[i], len);
-      (*types)[i] = kNoCompression;
-    }
+    if ((*types)[i] == kSnappyCompression)
+      out->append(comp, dense[i], keep_len[i]);
+    else
+      out->append(raw + offsets[i], off[i + 1] - off[i]);
     (*out_offsets)[i + 1] = out->size();
   }
   return Status::OK();
@@ -147,40 +143,43 @@ Status UncompressBlocks(int device, const char* data, const uint64_t* offsets, c
     std::string packed;
     packed.reserve(coff[m]);
     for (size_t j = 0; j < m; j++) packed.append(data + offsets[idx[j]], offsets[idx[j] + 1] - offsets[idx[j]]);
-    s = open_device(device);
+    SessionLease ss;
+    s = ss.Open(device);
     if (!s.ok()) return s;
-    DeviceScratch d;
-    if (d.stream.status() != hipSuccess) return hip_status(d.stream.status(), "stream");
-    const hipStream_t st = d.stream.get();
-    void *d_comp = nullptr, *d_coff = nullptr, *d_ulen = nullptr, *d_ok = nullptr;
-    hipError_t e = d.alloc(&d_comp, coff[m]);
-    if (e == hipSuccess) e = d.alloc(&d_coff, (m + 1) * sizeof(uint64_t));
-    if (e == hipSuccess) e = d.alloc(&d_ulen, m * sizeof(uint64_t));
-    if (e == hipSuccess) e = d.alloc(&d_ok, m);
-    if (e == hipSuccess) e = d.bounce.to_device(d_comp, packed.data(), coff[m], st);
-    if (e == hipSuccess) e = d.bounce.to_device(d_coff, coff.data(), (m + 1) * sizeof(uint64_t), st);
+    const hipStream_t st = ss->stream();
+    void *d_comp, *d_coff, *d_ulen, *d_ok;
+    hipError_t e = ss->scratch(0, coff[m], &d_comp);
+    if (e == hipSuccess) e = ss->scratch(1, (m + 1) * sizeof(uint64_t), &d_coff);
+    if (e == hipSuccess) e = ss->scratch(2, m * sizeof(uint64_t), &d_ulen);
+    if (e == hipSuccess) e = ss->scratch(3, m, &d_ok);
+    if (e == hipSuccess) e = ss->upload(d_comp, packed.data(), coff[m]);
+    if (e == hipSuccess) e = ss->upload(d_coff, coff.data(), (m + 1) * sizeof(uint64_t));
     if (e != hipSuccess) return hip_status(e, "staging");
     // GetUncompressedLength sizes the output windows
     if (lsbm_snappy_uncompressed_length_dev(d_comp, static_cast<const uint64_t*>(d_coff), m,
                                             static_cast<uint64_t*>(d_ulen), static_cast<uint8_t*>(d_ok),
                                             st) != LSBM_OK)
       return Status::IOError(lsbm_crc32c_last_error());
-    e = d.bounce.to_host(ulen.data(), d_ulen, m * sizeof(uint64_t), st);
-    if (e == hipSuccess) e = d.bounce.to_host(len_ok.data(), d_ok, m, st);
+    e = ss->download(ulen.data(), d_ulen, m * sizeof(uint64_t));
+    if (e == hipSuccess) e = ss->download(len_ok.data(), d_ok, m);
     if (e != hipSuccess) return hip_status(e, "uncompressed length");
-    for (size_t j = 0; j < m; j++) uoff[j + 1] = uoff[j] + (len_ok[j] ? ulen[j] : 0);
-    void *d_out = nullptr, *d_uoff = nullptr;
-    e = d.alloc(&d_out, uoff[m]);
-    if (e == hipSuccess) e = d.alloc(&d_uoff, (m + 1) * sizeof(uint64_t));
-    if (e == hipSuccess) e = d.bounce.to_device(d_uoff, uoff.data(), (m + 1) * sizeof(uint64_t), st);
+    for (size_t j = 0; j < m; j++) {
+      // a preamble no stream of this length can meet fails now, with no window
+      if (len_ok[j] && ulen[j] > kMaxExpansion * (coff[j + 1] - coff[j])) len_ok[j] = 0;
+      uoff[j + 1] = uoff[j] + (len_ok[j] ? ulen[j] : 0);
+    }
+    void *d_out, *d_uoff;
+    e = ss->scratch(4, uoff[m], &d_out);
+    if (e == hipSuccess) e = ss->scratch(5, (m + 1) * sizeof(uint64_t), &d_uoff);
+    if (e == hipSuccess) e = ss->upload(d_uoff, uoff.data(), (m + 1) * sizeof(uint64_t));
     if (e != hipSuccess) return hip_status(e, "staging");
     if (lsbm_snappy_uncompress_dev(d_comp, static_cast<const uint64_t*>(d_coff), m,
                                    static_cast<uint8_t*>(d_out), static_cast<const uint64_t*>(d_uoff),
                                    static_cast<uint8_t*>(d_ok), nullptr, st) != LSBM_OK)
       return Status::IOError(lsbm_crc32c_last_error());
     dec.assign(uoff[m], '\0');
-    e = d.bounce.to_host(dec_ok.data(), d_ok, m, st);
-    if (e == hipSuccess && uoff[m]) e = d.bounce.to_host(&dec[0], d_out, uoff[m], st);
+    e = ss->download(dec_ok.data(), d_ok, m);
+    if (e == hipSuccess && uoff[m]) e = ss->download(&dec[0], d_out, uoff[m]);
     if (e != hipSuccess) return hip_status(e, "uncompress");
   }
 

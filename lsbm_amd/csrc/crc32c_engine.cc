@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -20,6 +21,7 @@
 #include "crc32c_types.h"
 #include "engine_internal.h"
 #include "gf2.h"
+#include "host_session.h"
 
 namespace lsbm {
 
@@ -29,6 +31,8 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
                         const DevConsts* dc, int grid, hipStream_t stream);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, int grid, hipStream_t stream);
+hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint64_t* len, uint64_t n,
+                         uint8_t* dst, const uint64_t* dst_off, int grid, hipStream_t stream);
 hipError_t launch_stream_read(const void* buf, uint64_t nbytes, uint32_t* sink, int grid,
                               hipStream_t stream);
 
@@ -47,8 +51,12 @@ int fail(int code, const char* what) {
 
 constexpr int kMaxDevices = 64;
 
+// Per-device tables: built on first use, read-only until lsbm_crc32c_shutdown.
+// `ready` is the lock-free fast path of every call; `mu` serialises the
+// first initialisation (and shutdown) of a device.
 struct DeviceState {
-  std::once_flag once;
+  std::mutex mu;
+  std::atomic<bool> ready{false};
   int status = LSBM_ERR_NO_DEVICE;
   DevConsts* d_consts = nullptr;
   int num_cus = 0;
@@ -144,8 +152,14 @@ void init_device(int dev, DeviceState* st) {
 int ensure_device(int dev, DeviceState** out) {
   if (dev < 0 || dev >= kMaxDevices) return fail(LSBM_ERR_NO_DEVICE, "bad device ordinal");
   DeviceState* st = &g_dev[dev];
-  std::call_once(st->once, init_device, dev, st);
-  if (st->status != LSBM_OK) return st->status;
+  if (!st->ready.load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> l(st->mu);
+    if (!st->ready.load(std::memory_order_relaxed)) {
+      init_device(dev, st);
+      if (st->status != LSBM_OK) return st->status;
+      st->ready.store(true, std::memory_order_release);
+    }
+  }
   *out = st;
   return LSBM_OK;
 }
@@ -248,17 +262,6 @@ hipError_t reserve_slot(Slot& s, uint64_t bytes, uint64_t blocks) {
   return hipSuccess;
 }
 
-// Page-locked (hipHostMalloc'd or hipHostRegister'ed) host memory can be the
-// source of an async DMA as it is; pageable memory goes through staging.
-bool host_pinned(const void* p) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-    (void)hipGetLastError();  // clear the sticky "invalid value" for pageable memory
-    return false;
-  }
-  return attr.type == hipMemoryTypeHost;
-}
-
 // Copy blocks [first, last) of a pageable source into the pinned staging
 // buffer at their rebased offsets, on up to 8 threads for large chunks.
 void gather_blocks(uint8_t* dst, const uint64_t* rebased, const uint8_t* src,
@@ -314,6 +317,40 @@ __attribute__((visibility("default"))) const char* lsbm_crc32c_last_error(void) 
 __attribute__((visibility("default"))) int lsbm_crc32c_init(int device) {
   DeviceState* st = nullptr;
   return ensure_device(device, &st);
+}
+
+__attribute__((visibility("default"))) int lsbm_crc32c_shutdown(void) {
+  // the C++ layers' staging first (it synchronises its streams), then the
+  // host-staged batch slots and the per-device tables
+  HostSession::ShutdownAll();
+  int prev = 0;
+  const bool have_prev = hipGetDevice(&prev) == hipSuccess;
+  int rc = LSBM_OK;
+  for (int dev = 0; dev < kMaxDevices; dev++) {
+    DeviceState* st = &g_dev[dev];
+    std::lock_guard<std::mutex> l(st->mu);
+    Staging& stg = g_staging[dev];
+    std::lock_guard<std::mutex> ls(stg.mu);
+    if (!st->ready.load()) continue;
+    if (hipSetDevice(dev) != hipSuccess) {
+      rc = fail(LSBM_ERR_HIP, "hipSetDevice");
+      continue;
+    }
+    for (Slot& sl : stg.slot) {
+      if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+      free_slot_buffers(sl);
+      if (sl.done) (void)hipEventDestroy(sl.done);
+      if (sl.stream) (void)hipStreamDestroy(sl.stream);
+      sl = Slot();
+    }
+    (void)hipDeviceSynchronize();  // no kernel may still read the tables
+    if (st->d_consts) (void)hipFree(st->d_consts);
+    st->d_consts = nullptr;
+    st->status = LSBM_ERR_NO_DEVICE;
+    st->ready.store(false);
+  }
+  if (have_prev) (void)hipSetDevice(prev);
+  return rc;
 }
 
 __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
@@ -484,6 +521,27 @@ __attribute__((visibility("default"))) int lsbm_log_seal_dev(uint8_t* d_log, uin
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
+__attribute__((visibility("default"))) int lsbm_log_crcs_dev(const uint8_t* d_log,
+                                                             uint64_t log_bytes,
+                                                             const uint64_t* d_headers,
+                                                             uint64_t n_records,
+                                                             uint32_t* d_masked, uint32_t* d_nbad,
+                                                             void* stream) {
+  if (n_records == 0) return LSBM_OK;
+  if (!d_log || !d_headers || !d_masked) return fail(LSBM_ERR_INVALID, "null pointer");
+  RaggedArgs a = {};
+  a.base = d_log;
+  a.file = nullptr;  // the image is not written
+  a.handles = d_headers;
+  a.extents = kExtLogHeaders;
+  a.limit = log_bytes;
+  a.n = n_records;
+  a.out = d_masked;
+  a.nbad = d_nbad;
+  a.mode = kModeLogSeal;
+  return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
 __attribute__((visibility("default"))) int lsbm_log_verify_dev(const uint8_t* d_log,
                                                                uint64_t log_bytes,
                                                                const uint64_t* d_headers,
@@ -501,6 +559,22 @@ __attribute__((visibility("default"))) int lsbm_log_verify_dev(const uint8_t* d_
   a.nbad = d_nbad;
   a.mode = kModeLogVerify;
   return run_ragged(a, static_cast<hipStream_t>(stream));
+}
+
+__attribute__((visibility("default"))) int lsbm_gather_dev(const void* d_src, const uint64_t* d_src_off,
+                                                           const uint64_t* d_len, uint64_t n,
+                                                           void* d_dst, const uint64_t* d_dst_off,
+                                                           void* stream) {
+  if (n == 0) return LSBM_OK;
+  if (!d_src || !d_src_off || !d_len || !d_dst || !d_dst_off)
+    return fail(LSBM_ERR_INVALID, "null pointer");
+  DeviceState* st = nullptr;
+  int rc = current_device(&st);
+  if (rc != LSBM_OK) return rc;
+  hipError_t e = launch_gather(static_cast<const uint8_t*>(d_src), d_src_off, d_len, n,
+                               static_cast<uint8_t*>(d_dst), d_dst_off, st->num_cus * 8,
+                               static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LSBM_OK : fail_hip(e, "gather_kernel");
 }
 
 __attribute__((visibility("default"))) int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes,

@@ -532,11 +532,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
         t[3] = (uint8_t)(pend_v >> 16);
         t[4] = (uint8_t)(pend_v >> 24);
       } else if constexpr (mode == kModeLogSeal) {
-        uint8_t* h = reinterpret_cast<uint8_t*>(pend_a);
-        h[0] = (uint8_t)pend_v;
-        h[1] = (uint8_t)(pend_v >> 8);
-        h[2] = (uint8_t)(pend_v >> 16);
-        h[3] = (uint8_t)(pend_v >> 24);
+        if (args.file) {  // (null: the masked crcs only, lsbm_log_crcs_dev)
+          uint8_t* h = reinterpret_cast<uint8_t*>(pend_a);
+          h[0] = (uint8_t)pend_v;
+          h[1] = (uint8_t)(pend_v >> 8);
+          h[2] = (uint8_t)(pend_v >> 16);
+          h[3] = (uint8_t)(pend_v >> 24);
+        }
         if (args.out) args.out[b_lo + pend_i] = pend_v;
       } else if constexpr (mode == kModeOut || mode == kModeSstCrc) {
         *reinterpret_cast<uint32_t*>(pend_a) = pend_v;
@@ -824,6 +826,35 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
 }
 
 // ---------------------------------------------------------------------------
+// Gather: dst[dst_off[i], +len[i]) = src[src_off[i], +len[i]), one wave per
+// segment (grid-stride), 16-B stores where both sides allow, bytes elsewhere.
+// Compacts variable-length outputs before they go back to the host
+// (block_compression.cc: only the compressed bytes, not their capacity slots).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gather_kernel(const uint8_t* __restrict__ src,
+                                                     const uint64_t* __restrict__ src_off,
+                                                     const uint64_t* __restrict__ len, uint64_t n,
+                                                     uint8_t* __restrict__ dst,
+                                                     const uint64_t* __restrict__ dst_off) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t i = wave; i < n; i += nwaves) {
+    const uint8_t* a = src + src_off[i];
+    uint8_t* b = dst + dst_off[i];
+    const uint64_t m = len[i];
+    if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15u) == 0) {
+      const uint64_t m16 = m / 16;
+      for (uint64_t k = lane; k < m16; k += 64)
+        reinterpret_cast<u32x4*>(b)[k] = reinterpret_cast<const u32x4*>(a)[k];
+      for (uint64_t k = m16 * 16 + lane; k < m; k += 64) b[k] = a[k];
+    } else {
+      for (uint64_t k = lane; k < m; k += 64) b[k] = a[k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Benchmark helpers.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -939,6 +970,14 @@ hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
       return hipErrorInvalidValue;
   }
 #undef LSBM_LAUNCH_UNITS
+  return hipGetLastError();
+}
+
+hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint64_t* len, uint64_t n,
+                         uint8_t* dst, const uint64_t* dst_off, int grid, hipStream_t stream) {
+  const uint64_t want = (n + 3) / 4;
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(want < (uint64_t)grid ? want : grid)), dim3(256), 0,
+                     stream, src, src_off, len, n, dst, dst_off);
   return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@
 #include <string.h>
 
 #include "../../include/lsbm_bloom.h"
-#include "host_stage.h"
+#include "host_session.h"
 
 namespace lsbm {
 
@@ -20,46 +20,10 @@ namespace {
 
 constexpr uint64_t kFilterBase = 1ull << LSBM_FILTER_BASE_LG;  // table/filter_block.cc:14-16
 
-Status hip_status(hipError_t e, const char* what) {
-  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
 void put_fixed32(std::string* dst, uint32_t v) {  // util/coding.cc PutFixed32
   const char b[4] = {(char)(v & 0xff), (char)((v >> 8) & 0xff), (char)((v >> 16) & 0xff),
                      (char)(v >> 24)};
   dst->append(b, 4);
-}
-
-// Device buffers of one call, freed after the stream drains.
-struct DeviceArena {
-  std::vector<void*> ptrs;
-  PinnedBounce bounce;
-  CallStream stream;
-  ~DeviceArena() {
-    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
-    for (void* p : ptrs) (void)hipFree(p);
-  }
-  template <typename T>
-  hipError_t alloc(T** p, size_t count) {
-    void* q = nullptr;
-    const hipError_t e = hipMalloc(&q, count ? count * sizeof(T) : 1);
-    if (e == hipSuccess) ptrs.push_back(q);
-    *p = static_cast<T*>(q);
-    return e;
-  }
-  template <typename T>
-  hipError_t upload(T** d, const T* h, size_t count) {
-    hipError_t e = alloc(d, count);
-    if (e == hipSuccess && count) e = bounce.to_device(*d, h, count * sizeof(T), stream.get());
-    return e;
-  }
-};
-
-Status prepare(int device, DeviceArena* a) {
-  if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = a->stream.status();
-  return e == hipSuccess ? Status::OK() : hip_status(e, "device");
 }
 
 }  // namespace
@@ -124,22 +88,27 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
   first.push_back(key_offs.size() - 1);  // filters cover every key, in order
   std::vector<char> data(out_total);
   const size_t nf = out_off.size();
-  if (nf) {
-    DeviceArena a;
-    Status s = prepare(device, &a);
+  if (nf) {  // one launch on the device's session (host_session.h)
+    SessionLease ss;
+    Status s = ss.Open(device);
     if (!s.ok()) return s;
-    uint8_t *d_keys = nullptr, *d_out = nullptr;
-    uint64_t *d_offs = nullptr, *d_first = nullptr, *d_out_off = nullptr;
-    hipError_t e = a.upload(&d_keys, reinterpret_cast<const uint8_t*>(keys.data()), keys.size());
-    if (e == hipSuccess) e = a.upload(&d_offs, key_offs.data(), key_offs.size());
-    if (e == hipSuccess) e = a.upload(&d_first, first.data(), first.size());
-    if (e == hipSuccess) e = a.upload(&d_out_off, out_off.data(), out_off.size());
-    if (e == hipSuccess) e = a.alloc(&d_out, out_total);
+    void *d_keys, *d_offs, *d_first, *d_out_off, *d_out;
+    hipError_t e = ss->scratch(0, keys.size(), &d_keys);
+    if (e == hipSuccess) e = ss->scratch(1, key_offs.size() * sizeof(uint64_t), &d_offs);
+    if (e == hipSuccess) e = ss->scratch(2, first.size() * sizeof(uint64_t), &d_first);
+    if (e == hipSuccess) e = ss->scratch(3, out_off.size() * sizeof(uint64_t), &d_out_off);
+    if (e == hipSuccess) e = ss->scratch(4, out_total, &d_out);
+    if (e == hipSuccess) e = ss->upload(d_keys, keys.data(), keys.size());
+    if (e == hipSuccess) e = ss->upload(d_offs, key_offs.data(), key_offs.size() * sizeof(uint64_t));
+    if (e == hipSuccess) e = ss->upload(d_first, first.data(), first.size() * sizeof(uint64_t));
+    if (e == hipSuccess) e = ss->upload(d_out_off, out_off.data(), out_off.size() * sizeof(uint64_t));
     if (e != hipSuccess) return hip_status(e, "staging");
-    if (lsbm_bloom_build_dev(d_keys, d_offs, internal ? LSBM_INTERNAL_KEY_SUFFIX : 0, d_first,
-                             d_out_off, nf, bpk, d_out, a.stream.get()) != LSBM_OK)
+    if (lsbm_bloom_build_dev(static_cast<const uint8_t*>(d_keys), static_cast<const uint64_t*>(d_offs),
+                             internal ? LSBM_INTERNAL_KEY_SUFFIX : 0,
+                             static_cast<const uint64_t*>(d_first), static_cast<const uint64_t*>(d_out_off),
+                             nf, bpk, static_cast<uint8_t*>(d_out), ss->stream()) != LSBM_OK)
       return Status::IOError(lsbm_crc32c_last_error());
-    e = a.bounce.to_host(data.data(), d_out, out_total, a.stream.get());
+    e = ss->download(data.data(), d_out, out_total);
     if (e != hipSuccess) return hip_status(e, "filters");
   }
   for (size_t t = 0; t < n; t++) {  // :41-49
@@ -161,8 +130,8 @@ Status FilterBlockReader::KeyMayMatch(int device, const uint64_t* block_offsets,
   may->assign(n, 1);
   if (n == 0) return Status::OK();
   if (!block_offsets || !keys || !key_offsets) return Status::InvalidArgument("null pointer");
-  DeviceArena a;
-  Status s = prepare(device, &a);
+  SessionLease ss;
+  Status s = ss.Open(device);
   if (!s.ok()) return s;
   std::vector<uint64_t> handles(2 * n), offs(n + 1);
   for (size_t i = 0; i < n; i++) {
@@ -170,22 +139,29 @@ Status FilterBlockReader::KeyMayMatch(int device, const uint64_t* block_offsets,
     handles[2 * i + 1] = size_;
   }
   for (size_t i = 0; i <= n; i++) offs[i] = key_offsets[i] - key_offsets[0];
-  uint8_t *d_block = nullptr, *d_keys = nullptr, *d_may = nullptr;
-  uint64_t *d_handles = nullptr, *d_data = nullptr, *d_offs = nullptr;
-  hipError_t e = a.upload(&d_block, reinterpret_cast<const uint8_t*>(contents_), size_);
-  if (e == hipSuccess) e = a.upload(&d_handles, handles.data(), handles.size());
-  if (e == hipSuccess) e = a.upload(&d_data, block_offsets, n);
-  if (e == hipSuccess)
-    e = a.upload(&d_keys, reinterpret_cast<const uint8_t*>(keys + key_offsets[0]), offs[n]);
-  if (e == hipSuccess) e = a.upload(&d_offs, offs.data(), offs.size());
-  if (e == hipSuccess) e = a.alloc(&d_may, n);
+  void *d_block, *d_keys, *d_may, *d_handles, *d_data, *d_offs;
+  hipError_t e = ss->scratch(0, size_, &d_block);
+  if (e == hipSuccess) e = ss->scratch(1, handles.size() * sizeof(uint64_t), &d_handles);
+  if (e == hipSuccess) e = ss->scratch(2, n * sizeof(uint64_t), &d_data);
+  if (e == hipSuccess) e = ss->scratch(3, offs[n], &d_keys);
+  if (e == hipSuccess) e = ss->scratch(4, offs.size() * sizeof(uint64_t), &d_offs);
+  if (e == hipSuccess) e = ss->scratch(5, n, &d_may);
+  if (e == hipSuccess) e = ss->upload(d_block, contents_, size_);
+  if (e == hipSuccess) e = ss->upload(d_handles, handles.data(), handles.size() * sizeof(uint64_t));
+  if (e == hipSuccess) e = ss->upload(d_data, block_offsets, n * sizeof(uint64_t));
+  if (e == hipSuccess) e = ss->upload(d_keys, keys + key_offsets[0], offs[n]);
+  if (e == hipSuccess) e = ss->upload(d_offs, offs.data(), offs.size() * sizeof(uint64_t));
   if (e != hipSuccess) return hip_status(e, "staging");
-  if (lsbm_filter_block_may_match_dev(d_block, d_handles, d_data, d_keys, d_offs,
+  if (lsbm_filter_block_may_match_dev(static_cast<const uint8_t*>(d_block),
+                                      static_cast<const uint64_t*>(d_handles),
+                                      static_cast<const uint64_t*>(d_data),
+                                      static_cast<const uint8_t*>(d_keys),
+                                      static_cast<const uint64_t*>(d_offs),
                                       options_.internal_keys ? LSBM_INTERNAL_KEY_SUFFIX : 0, n,
-                                      options_.bits_per_key, options_.bloom_bits_use, d_may,
-                                      nullptr, a.stream.get()) != LSBM_OK)
+                                      options_.bits_per_key, options_.bloom_bits_use,
+                                      static_cast<uint8_t*>(d_may), nullptr, ss->stream()) != LSBM_OK)
     return Status::IOError(lsbm_crc32c_last_error());
-  e = a.bounce.to_host(may->data(), d_may, n, a.stream.get());
+  e = ss->download(may->data(), d_may, n);
   return e == hipSuccess ? Status::OK() : hip_status(e, "lookups");
 }
 

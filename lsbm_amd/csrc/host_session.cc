@@ -1,0 +1,292 @@
+// host_session.cc -- see host_session.h.
+#include "host_session.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/lsbm_crc32c.h"
+
+namespace lsbm {
+
+Status hip_status(hipError_t e, const char* what) {
+  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t attr;
+  if (!p || hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" for pageable memory
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// ---- copy-thread pool: one job at a time, the caller works on it too ----
+namespace {
+
+class CopyPool {
+ public:
+  void run(void* dst, const void* src, size_t n) {
+    std::lock_guard<std::mutex> job(job_mu_);
+    start();
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      dst_ = static_cast<char*>(dst);
+      src_ = static_cast<const char*>(src);
+      n_ = n;
+      pieces_ = (n + kPiece - 1) / kPiece;
+      next_ = finished_ = 0;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return finished_ == pieces_; });
+  }
+
+ private:
+  static constexpr size_t kPiece = 1u << 20;
+  void start() {
+    if (!threads_.empty()) return;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    // (the caller is the 16th: the one-GPU box's CPU share is 16)
+    const unsigned nt = std::min(15u, hw > 1 ? hw - 1 : 1u);
+    for (unsigned t = 0; t < nt; t++)
+      threads_.emplace_back([this] {
+        uint64_t seen = 0;
+        for (;;) {
+          {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [&] { return gen_ != seen; });
+            seen = gen_;
+          }
+          work();
+        }
+      });
+    for (auto& t : threads_) t.detach();  // parked on cv_ for the life of the process
+  }
+  void work() {
+    for (;;) {
+      size_t k;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        if (next_ >= pieces_) return;
+        k = next_++;
+      }
+      const size_t off = k * kPiece, len = std::min(kPiece, n_ - off);
+      memcpy(dst_ + off, src_ + off, len);
+      std::lock_guard<std::mutex> l(mu_);
+      if (++finished_ == pieces_) done_cv_.notify_all();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> threads_;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t n_ = 0, pieces_ = 0, next_ = 0, finished_ = 0;
+  uint64_t gen_ = 0;
+};
+
+CopyPool* pool() {
+  static CopyPool* p = new CopyPool;  // never destroyed: its threads outlive static teardown
+  return p;
+}
+
+constexpr int kMaxDevices = 64;
+std::mutex g_reg;
+HostSession* g_sessions[kMaxDevices] = {};
+
+}  // namespace
+
+void parallel_copy(void* dst, const void* src, size_t n) {
+  if (n < (4u << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  pool()->run(dst, src, n);
+}
+
+// ---- buffers ----
+hipError_t StagePair::reserve(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  release();
+  bytes = std::max<size_t>(bytes, 1u << 16);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), bytes);
+  if (e != hipSuccess) {
+    release();
+    return e;
+  }
+  cap = bytes;
+  return hipSuccess;
+}
+
+void StagePair::release() {
+  if (h) (void)hipHostFree(h);
+  if (d) (void)hipFree(d);
+  h = d = nullptr;
+  cap = 0;
+}
+
+// ---- session ----
+hipError_t HostSession::init() {
+  for (Stage& s : stage_) {
+    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+HostSession::~HostSession() {
+  DeviceGuard g(device_);
+  for (Stage& s : stage_) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    s.bulk.release();
+    s.meta.release();
+    s.res.release();
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  for (int k = 0; k < kScratch; k++)
+    if (scratch_[k]) (void)hipFree(scratch_[k]);
+}
+
+hipError_t HostSession::scratch(int k, size_t bytes, void** p) {
+  if (bytes > scratch_cap_[k]) {
+    if (scratch_[k]) {
+      (void)hipStreamSynchronize(stage_[0].stream);
+      (void)hipFree(scratch_[k]);
+      scratch_[k] = nullptr;
+      scratch_cap_[k] = 0;
+    }
+    const size_t cap = std::max<size_t>(bytes, 1u << 12);
+    const hipError_t e = hipMalloc(&scratch_[k], cap);
+    if (e != hipSuccess) return e;
+    scratch_cap_[k] = cap;
+  }
+  *p = scratch_[k];
+  return hipSuccess;
+}
+
+hipError_t HostSession::wait(Stage& s) {
+  if (!s.busy) return hipSuccess;
+  s.busy = false;
+  return hipEventSynchronize(s.done);
+}
+
+hipError_t HostSession::upload(void* d, const void* h, size_t n) {
+  if (n == 0) return hipSuccess;
+  Stage& s0 = stage_[0];
+  if (host_pinned(h)) {
+    hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s0.stream);
+    return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
+  }
+  // through the stages' pinned buffers: stage i's copy overlaps stage i-1's
+  // DMA (on the other stages' streams, so stage 0's queue is drained first)
+  hipError_t e0 = hipStreamSynchronize(s0.stream);
+  if (e0 != hipSuccess) return e0;
+  int i = 0;
+  for (size_t off = 0; off < n; off += kChunkBytes, i = (i + 1) % kStages) {
+    const size_t k = std::min(kChunkBytes, n - off);
+    Stage& s = stage_[i];
+    hipError_t e = wait(s);
+    if (e == hipSuccess) e = s.bulk.reserve(kChunkBytes);
+    if (e != hipSuccess) return e;
+    parallel_copy(s.bulk.h, static_cast<const char*>(h) + off, k);
+    e = hipMemcpyAsync(static_cast<char*>(d) + off, s.bulk.h, k, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) return e;
+    s.busy = true;
+  }
+  for (Stage& s : stage_) {
+    const hipError_t e = wait(s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t HostSession::download(void* h, const void* d, size_t n) {
+  if (n == 0) return hipSuccess;
+  Stage& s0 = stage_[0];
+  // (everything the caller enqueued on stage 0's stream comes first)
+  if (host_pinned(h)) {
+    hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s0.stream);
+    return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
+  }
+  hipError_t e = hipStreamSynchronize(s0.stream);
+  if (e != hipSuccess) return e;
+  const size_t chunks = (n + kChunkBytes - 1) / kChunkBytes;
+  auto issue = [&](size_t c) -> hipError_t {
+    Stage& s = stage_[c % kStages];
+    const size_t off = c * kChunkBytes, k = std::min(kChunkBytes, n - off);
+    hipError_t ee = s.bulk.reserve(kChunkBytes);
+    if (ee == hipSuccess)
+      ee = hipMemcpyAsync(s.bulk.h, static_cast<const char*>(d) + off, k, hipMemcpyDeviceToHost,
+                          s.stream);
+    if (ee == hipSuccess) ee = hipEventRecord(s.done, s.stream);
+    if (ee == hipSuccess) s.busy = true;
+    return ee;
+  };
+  for (size_t c = 0; c < chunks && c < (size_t)kStages; c++)
+    if ((e = issue(c)) != hipSuccess) return e;
+  for (size_t c = 0; c < chunks; c++) {
+    Stage& s = stage_[c % kStages];
+    if ((e = wait(s)) != hipSuccess) return e;
+    const size_t off = c * kChunkBytes, k = std::min(kChunkBytes, n - off);
+    parallel_copy(static_cast<char*>(h) + off, s.bulk.h, k);
+    if (c + kStages < chunks && (e = issue(c + kStages)) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+void HostSession::ShutdownAll() {
+  std::lock_guard<std::mutex> l(g_reg);
+  for (int dev = 0; dev < kMaxDevices; dev++) {
+    HostSession* s = g_sessions[dev];
+    if (!s) continue;
+    {
+      std::lock_guard<std::mutex> sl(s->mu_);  // no lease may be open
+    }
+    delete s;
+    g_sessions[dev] = nullptr;
+  }
+}
+
+// ---- lease ----
+SessionLease::~SessionLease() {
+  if (lock_.owns_lock()) lock_.unlock();
+  delete guard_;
+}
+
+Status SessionLease::Open(int device) {
+  if (device < 0 || device >= kMaxDevices) return Status::InvalidArgument("bad device ordinal");
+  if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+  guard_ = new DeviceGuard(device);
+  if (guard_->status() != hipSuccess) return hip_status(guard_->status(), "hipSetDevice");
+  HostSession* s = nullptr;
+  {
+    std::lock_guard<std::mutex> l(g_reg);
+    s = g_sessions[device];
+    if (!s) {
+      s = new HostSession(device);
+      const hipError_t e = s->init();  // streams on `device` (current)
+      if (e != hipSuccess) {
+        delete s;
+        return hip_status(e, "session streams");
+      }
+      g_sessions[device] = s;
+    }
+  }
+  lock_ = std::unique_lock<std::mutex>(s->mu_);
+  s_ = s;
+  return Status::OK();
+}
+
+}  // namespace lsbm

@@ -1,0 +1,141 @@
+// host_session.h -- persistent per-device staging for the C++ host layers
+// (table_checksum.cc, log_checksum.cc, filter_block.cc, block_compression.cc)
+// and the host-staged batch entry point (crc32c_engine.cc).
+//
+// A HostSession belongs to one device and is created on that device the
+// first time a layer uses it: kStages pipeline stages, each a non-blocking
+// stream, a completion event and three pinned-host / device buffer pairs
+// (bulk bytes, per-item inputs, per-item results) that grow on demand and are
+// kept, plus a few device scratch buffers for single-shot layers.  Nothing is
+// allocated per call once the buffers have reached their working size;
+// lsbm_crc32c_shutdown() frees everything.
+//
+// Copies into pinned memory are the host's share of the work: copies of 4 MiB
+// and more are split over a pool of copy threads so that the staging
+// keeps up with PCIe (~55 GB/s measured for pinned H2D on the MI355X box).
+// A source that is already page-locked (hipHostMalloc / hipHostRegister) is
+// DMA-ed directly.  All DMA is stream-ordered hipMemcpyAsync on the stage's
+// stream: a synchronous hipMemcpy from pageable memory may return before its
+// DMA has landed and is not ordered with a non-blocking stream (the stale-
+// bytes race DESIGN.md section 5 records).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <mutex>
+
+#include "../../include/lsbm/status.h"
+
+namespace lsbm {
+
+// Makes `device` current for a scope and restores the caller's device after.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    have_prev_ = hipGetDevice(&prev_) == hipSuccess;
+    err_ = hipSetDevice(device);
+  }
+  ~DeviceGuard() {
+    if (have_prev_) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+  hipError_t status() const { return err_; }
+
+ private:
+  int prev_ = 0;
+  bool have_prev_ = false;
+  hipError_t err_;
+};
+
+// A pinned host buffer and a device buffer of the same capacity.
+struct StagePair {
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes);  // grows (never shrinks); contents are not kept
+  void release();
+};
+
+// One pipeline stage.
+struct Stage {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  bool busy = false;  // work enqueued whose results the caller has not collected
+  uint64_t tag = 0;   // the caller's chunk number
+  StagePair bulk, meta, res;
+};
+
+class HostSession {
+ public:
+  static constexpr int kStages = 3;
+  static constexpr size_t kChunkBytes = 64u << 20;  // bulk bytes per stage and chunk (at most)
+  static constexpr size_t kMinChunkBytes = 4u << 20;
+  // Chunk size for a job of `total` bytes: about a quarter of it, so that even
+  // one table's copy, DMA and kernel overlap, within [4 MiB, 64 MiB].
+  static size_t chunk_for(size_t total) {
+    const size_t q = total / 4;
+    return q < kMinChunkBytes ? kMinChunkBytes : (q > kChunkBytes ? kChunkBytes : q);
+  }
+  static constexpr int kScratch = 8;
+
+  Stage& stage(int i) { return stage_[i]; }
+  // Device scratch buffer k (k < kScratch), at least `bytes` long.
+  hipError_t scratch(int k, size_t bytes, void** p);
+  hipStream_t stream() const { return stage_[0].stream; }
+  int device() const { return device_; }
+
+  // Host -> device / device -> host of n bytes on stage 0's stream, through
+  // the stages' pinned buffers (overlapped) unless `h` is page-locked.
+  // Synchronous: returns when the bytes have arrived.
+  hipError_t upload(void* d, const void* h, size_t n);
+  hipError_t download(void* h, const void* d, size_t n);
+
+  // Waits for a stage's enqueued work (no-op if idle); clears busy.
+  hipError_t wait(Stage& s);
+
+  // Frees every session (lsbm_crc32c_shutdown).
+  static void ShutdownAll();
+
+ private:
+  friend class SessionLease;
+  explicit HostSession(int device) : device_(device) {}
+  ~HostSession();
+  hipError_t init();
+  int device_;
+  std::mutex mu_;
+  Stage stage_[kStages];
+  void* scratch_[kScratch] = {};
+  size_t scratch_cap_[kScratch] = {};
+};
+
+// The device's session, locked for this caller, with the device current for
+// the lease's lifetime (the caller's current device is restored after).
+class SessionLease {
+ public:
+  SessionLease() = default;
+  ~SessionLease();
+  SessionLease(const SessionLease&) = delete;
+  SessionLease& operator=(const SessionLease&) = delete;
+  // Initialises the device (lsbm_crc32c_init) and its session.
+  Status Open(int device);
+  HostSession* operator->() const { return s_; }
+  HostSession& operator*() const { return *s_; }
+
+ private:
+  HostSession* s_ = nullptr;
+  DeviceGuard* guard_ = nullptr;
+  std::unique_lock<std::mutex> lock_;
+};
+
+// Is p inside page-locked host memory (hipHostMalloc'd or registered)?
+bool host_pinned(const void* p);
+
+// memcpy of n bytes, split over the copy-thread pool when n >= 4 MiB.
+void parallel_copy(void* dst, const void* src, size_t n);
+
+// Status for a failed HIP call.
+Status hip_status(hipError_t e, const char* what);
+
+}  // namespace lsbm

@@ -13,49 +13,97 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "../../include/lsbm_crc32c.h"
-#include "host_stage.h"
+#include "host_session.h"
 
 namespace lsbm {
 namespace log {
 
 namespace {
 
-Status hip_status(hipError_t e, const char* what) {
-  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
-}
 
-struct DeviceLog {
-  uint8_t* image = nullptr;
-  uint64_t* headers = nullptr;
-  void* aux = nullptr;  // masked CRCs (seal) or ok flags (verify)
-  uint32_t* nbad = nullptr;
-  PinnedBounce bounce;
-  CallStream stream;
-  ~DeviceLog() {
-    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
-    if (image) (void)hipFree(image);
-    if (headers) (void)hipFree(headers);
-    if (aux) (void)hipFree(aux);
-    if (nbad) (void)hipFree(nbad);
+// The CRC work of a log image through the device's HostSession stages
+// (host_session.h), three chunks in flight.  Records [0, n) have their headers
+// at heads[] (ascending, inside [lo, hi)); chunks are the image's 4-64 MiB
+// windows, and physical records never cross a 32 KiB log block
+// (common/log_writer.cc:33-40), so none crosses a window.  seal: res[4i..] =
+// the masked crc of record i (lsbm_log_crcs_dev, the image on the device is
+// not written); verify: res[i] = its checksum verdict (lsbm_log_verify_dev).
+Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint64_t* heads,
+               size_t n, bool seal, uint8_t* res) {
+  if (n == 0) return Status::OK();
+  struct Chunk {
+    uint64_t lo, hi;
+    size_t first, count;
+  };
+  // windows of a multiple of kBlockSize, so that no record crosses one
+  const uint64_t kLogChunk = HostSession::chunk_for(hi - lo) / kBlockSize * kBlockSize;
+  std::vector<Chunk> chunks;
+  for (size_t i = 0; i < n;) {
+    const uint64_t w = heads[i] / kLogChunk;
+    Chunk c{std::max(lo, w * kLogChunk), std::min(hi, (w + 1) * kLogChunk), i, 0};
+    while (i < n && heads[i] / kLogChunk == w) i++, c.count++;
+    chunks.push_back(c);
   }
-};
-
-// Stage image[0, n) and the header offsets on `device` (host_stage.h).
-Status stage(int device, const char* image, size_t n, const uint64_t* headers, size_t count,
-             size_t aux_bytes, DeviceLog* d) {
-  if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = d->stream.status();
-  if (e == hipSuccess) e = hipMalloc(&d->image, n ? n : 1);
-  if (e == hipSuccess) e = hipMalloc(&d->headers, count * sizeof(uint64_t));
-  if (e == hipSuccess) e = hipMalloc(&d->aux, aux_bytes);
-  if (e == hipSuccess) e = hipMalloc(&d->nbad, sizeof(uint32_t));
-  if (e == hipSuccess) e = d->bounce.to_device(d->image, image, n, d->stream.get());
-  if (e == hipSuccess)
-    e = d->bounce.to_device(d->headers, headers, count * sizeof(uint64_t), d->stream.get());
-  if (e == hipSuccess) e = hipMemsetAsync(d->nbad, 0, sizeof(uint32_t), d->stream.get());
-  return e == hipSuccess ? Status::OK() : hip_status(e, "staging");
+  const bool pinned = host_pinned(img);
+  SessionLease s;
+  Status st = s.Open(device);
+  if (!st.ok()) return st;
+  const size_t per = seal ? 4 : 1;
+  auto finish = [&](Stage& sg) -> Status {
+    const hipError_t e = s->wait(sg);
+    if (e != hipSuccess) return hip_status(e, seal ? "seal" : "verify");
+    const Chunk& c = chunks[sg.tag];
+    memcpy(res + c.first * per, sg.res.h, c.count * per);
+    return Status::OK();
+  };
+  for (size_t k = 0; k < chunks.size(); k++) {
+    Stage& sg = s->stage((int)(k % HostSession::kStages));
+    if (sg.busy) {
+      st = finish(sg);
+      if (!st.ok()) return st;
+    }
+    const Chunk& c = chunks[k];
+    const uint64_t bytes = c.hi - c.lo;
+    hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
+    if (e == hipSuccess) e = sg.meta.reserve(c.count * sizeof(uint64_t));
+    if (e == hipSuccess) e = sg.res.reserve(c.count * per);
+    if (e != hipSuccess) return hip_status(e, "staging buffers");
+    uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
+    for (size_t i = 0; i < c.count; i++) hh[i] = heads[c.first + i] - c.lo;
+    if (pinned) {
+      e = hipMemcpyAsync(sg.bulk.d, img + c.lo, bytes, hipMemcpyHostToDevice, sg.stream);
+    } else {
+      parallel_copy(sg.bulk.h, img + c.lo, bytes);
+      e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, bytes, hipMemcpyHostToDevice, sg.stream);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(sg.meta.d, sg.meta.h, c.count * sizeof(uint64_t), hipMemcpyHostToDevice,
+                         sg.stream);
+    if (e != hipSuccess) return hip_status(e, "H2D");
+    const uint64_t* d_h = reinterpret_cast<const uint64_t*>(sg.meta.d);
+    const int rc = seal ? lsbm_log_crcs_dev(sg.bulk.d, bytes, d_h, c.count,
+                                            reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream)
+                        : lsbm_log_verify_dev(sg.bulk.d, bytes, d_h, c.count, sg.res.d, nullptr,
+                                              sg.stream);
+    if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+    e = hipMemcpyAsync(sg.res.h, sg.res.d, c.count * per, hipMemcpyDeviceToHost, sg.stream);
+    if (e == hipSuccess) e = hipEventRecord(sg.done, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "D2H");
+    sg.busy = true;
+    sg.tag = k;
+  }
+  for (size_t k = chunks.size() > (size_t)HostSession::kStages ? chunks.size() - HostSession::kStages : 0;
+       k < chunks.size(); k++) {
+    Stage& sg = s->stage((int)(k % HostSession::kStages));
+    if (sg.busy) {
+      st = finish(sg);
+      if (!st.ok()) return st;
+    }
+  }
+  return Status::OK();
 }
 
 inline uint32_t header_length(const uint8_t* h) { return (uint32_t)h[4] | ((uint32_t)h[5] << 8); }
@@ -280,24 +328,13 @@ void BatchWriter::AddRecord(const char* data, size_t n) {
 Status BatchWriter::Seal(int device) {
   const size_t count = headers_.size() - sealed_;
   if (count == 0) return Status::OK();
-  // stage only the unsealed tail of the log, headers rebased to it
-  const uint64_t base = headers_[sealed_];
-  std::vector<uint64_t> rebased(count);
-  for (size_t i = 0; i < count; i++) rebased[i] = headers_[sealed_ + i] - base;
-  DeviceLog d;
-  Status s = stage(device, dest_.data() + base, dest_.size() - base, rebased.data(), count,
-                   count * sizeof(uint32_t), &d);
-  if (!s.ok()) return s;
-  if (lsbm_log_seal_dev(d.image, dest_.size() - base, d.headers, count,
-                        static_cast<uint32_t*>(d.aux), d.nbad, d.stream.get()) != LSBM_OK)
-    return Status::IOError(lsbm_crc32c_last_error());
+  // the unsealed tail of the log: every pending header's masked crc (4 B each
+  // come back), EncodeFixed32 into its header (util/coding.cc)
   std::vector<uint32_t> masked(count);
-  uint32_t nbad = 0;
-  hipError_t e = d.bounce.to_host(masked.data(), d.aux, count * sizeof(uint32_t), d.stream.get());
-  if (e == hipSuccess) e = d.bounce.to_host(&nbad, d.nbad, sizeof(nbad), d.stream.get());
-  if (e != hipSuccess) return hip_status(e, "seal");
-  if (nbad) return Status::Corruption("log record outside the image");  // cannot happen
-  for (size_t i = 0; i < count; i++) {  // EncodeFixed32 (util/coding.cc)
+  Status s = run_log(device, dest_.data(), headers_[sealed_], dest_.size(), &headers_[sealed_],
+                     count, true, reinterpret_cast<uint8_t*>(masked.data()));
+  if (!s.ok()) return s;
+  for (size_t i = 0; i < count; i++) {
     char* h = &dest_[headers_[sealed_ + i]];
     for (int k = 0; k < 4; k++) h[k] = (char)(masked[i] >> (8 * k));
   }
@@ -324,15 +361,9 @@ Status BatchReader::Verify(int device) {
     }
   }
   ok_.assign(headers_.size(), 0);
-  if (!headers_.empty()) {  // one GPU batch for all of them
-    DeviceLog d;
-    Status s = stage(device, file_, size_, headers_.data(), headers_.size(), headers_.size(), &d);
+  if (!headers_.empty()) {  // one pipelined GPU pass over all of them
+    Status s = run_log(device, file_, 0, size_, headers_.data(), headers_.size(), false, ok_.data());
     if (!s.ok()) return s;
-    if (lsbm_log_verify_dev(d.image, size_, d.headers, headers_.size(),
-                            static_cast<uint8_t*>(d.aux), d.nbad, d.stream.get()) != LSBM_OK)
-      return Status::IOError(lsbm_crc32c_last_error());
-    hipError_t e = d.bounce.to_host(ok_.data(), d.aux, headers_.size(), d.stream.get());
-    if (e != hipSuccess) return hip_status(e, "verify");
   }
   // pass 2 (ReadRecord): the reader itself, with the GPU's verdicts
   walk_ = new Walk(img, size_, initial_offset_, reporter_, nullptr, &headers_, &ok_);

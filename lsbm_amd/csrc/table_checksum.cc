@@ -1,14 +1,22 @@
 // table_checksum.cc -- include/lsbm/table_checksum.h on top of the C ABI.
-// The file image is staged to the device once, sealed or verified there by
-// the ragged kernel in its SSTable modes, and the trailers (seal) or the
-// per-block flags (verify) come back.
+//
+// The blocks of one or many table images are packed into chunks of at most
+// 64 MiB of whole blocks (with their trailers), and the chunks run through
+// the device's persistent HostSession stages (host_session.h), three deep:
+// while chunk c's bytes cross PCIe, chunk c-1 is checksummed and chunk c-2's
+// results come back.  Only 4 B (seal: the masked trailer crc, dense, written
+// into the host image by the host) or 1 B (verify: the ok flag) per block
+// return to the host, never the image.
 #include "../../include/lsbm/table_checksum.h"
 
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 
+#include <algorithm>
+#include <numeric>
+
 #include "../../include/lsbm_crc32c.h"
-#include "host_stage.h"
+#include "host_session.h"
 
 namespace lsbm {
 
@@ -25,26 +33,6 @@ std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64
 
 namespace {
 
-struct DeviceBuffers {
-  uint8_t* file = nullptr;
-  uint64_t* handles = nullptr;
-  uint8_t* aux = nullptr;   // types (seal) or ok flags (verify)
-  uint32_t* nbad = nullptr;
-  PinnedBounce bounce;
-  CallStream stream;
-  ~DeviceBuffers() {
-    if (stream.status() == hipSuccess) (void)hipStreamSynchronize(stream.get());
-    if (file) (void)hipFree(file);
-    if (handles) (void)hipFree(handles);
-    if (aux) (void)hipFree(aux);
-    if (nbad) (void)hipFree(nbad);
-  }
-};
-
-Status hip_status(hipError_t e, const char* what) {
-  return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
 Status check_handles(size_t file_size, const BlockHandle* h, size_t n) {
   for (size_t i = 0; i < n; i++)
     if (h[i].offset > file_size || h[i].size > file_size - h[i].offset ||
@@ -53,44 +41,228 @@ Status check_handles(size_t file_size, const BlockHandle* h, size_t n) {
   return Status::OK();
 }
 
-// Stage file + handles (+ aux bytes) on `device` (host_stage.h).
-Status stage(int device, const void* file, size_t file_size, const BlockHandle* h, size_t n,
-             const uint8_t* aux_in, DeviceBuffers* d) {
-  int rc = lsbm_crc32c_init(device);
-  if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = d->stream.status();
-  if (e == hipSuccess) e = hipMalloc(&d->file, file_size ? file_size : 1);
-  if (e == hipSuccess) e = hipMalloc(&d->handles, n * sizeof(BlockHandle));
-  if (e == hipSuccess) e = hipMalloc(&d->aux, n);
-  if (e == hipSuccess) e = hipMalloc(&d->nbad, sizeof(uint32_t));
-  hipStream_t s = d->stream.get();
-  if (e == hipSuccess) e = d->bounce.to_device(d->file, file, file_size, s);
-  if (e == hipSuccess) e = d->bounce.to_device(d->handles, h, n * sizeof(BlockHandle), s);  // {offset,size}
-  if (e == hipSuccess && aux_in) e = d->bounce.to_device(d->aux, aux_in, n, s);
-  if (e == hipSuccess) e = hipMemsetAsync(d->nbad, 0, sizeof(uint32_t), s);
-  return e == hipSuccess ? Status::OK() : hip_status(e, "staging");
+// Bytes [lo, hi) of table t, holding its blocks order[first, first + count).
+struct Piece {
+  uint32_t t;
+  uint64_t lo, hi;
+  size_t first, count;
+  uint64_t dst;  // offset in the chunk
+};
+struct Chunk {
+  std::vector<Piece> pieces;
+  uint64_t bytes = 0;
+  size_t blocks = 0;
+};
+
+struct Plan {
+  std::vector<std::vector<size_t>> order;  // per table: block indices by offset
+  std::vector<Chunk> chunks;
+  size_t max_blocks = 0;
+};
+
+// Whole blocks (and trailers) in offset order, packed into chunks of at most
+// HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own).
+void make_plan(const TableImage* tables, size_t count, Plan* p) {
+  p->order.resize(count);
+  size_t total = 0;
+  for (size_t t = 0; t < count; t++) total += tables[t].file_size;
+  const size_t limit = HostSession::chunk_for(total);
+  Chunk cur;
+  auto close = [&]() {
+    if (cur.blocks == 0) return;
+    p->max_blocks = std::max(p->max_blocks, cur.blocks);
+    p->chunks.push_back(std::move(cur));
+    cur = Chunk();
+  };
+  for (size_t t = 0; t < count; t++) {
+    const TableImage& tb = tables[t];
+    std::vector<size_t>& ord = p->order[t];
+    ord.resize(tb.n);
+    std::iota(ord.begin(), ord.end(), 0);
+    bool sorted = true;
+    for (size_t i = 1; i < tb.n && sorted; i++)
+      sorted = tb.handles[i].offset >= tb.handles[i - 1].offset;
+    if (!sorted)
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        return tb.handles[a].offset < tb.handles[b].offset;
+      });
+    bool open = false;  // cur.pieces.back() is this table's and may grow
+    for (size_t k = 0; k < tb.n; k++) {
+      const BlockHandle& h = tb.handles[ord[k]];
+      const uint64_t end = h.offset + h.size + kBlockTrailerSize;
+      if (open) {
+        Piece& pc = cur.pieces.back();
+        const uint64_t hi = std::max(pc.hi, end);
+        if (cur.bytes + (hi - pc.hi) <= limit) {
+          cur.bytes += hi - pc.hi;
+          pc.hi = hi;
+          pc.count++;
+          cur.blocks++;
+          continue;
+        }
+        close();
+      }
+      if (cur.blocks && cur.bytes + (end - h.offset) > limit) close();
+      cur.pieces.push_back(Piece{(uint32_t)t, h.offset, end, k, 1, cur.bytes});
+      cur.bytes += end - h.offset;
+      cur.blocks++;
+      open = true;
+    }
+  }
+  close();
+}
+
+enum class Op { kSeal, kVerify };
+
+// The pipeline.  Seal: trailers written into the host images.  Verify: ok[]
+// per block, concatenated over the tables in their block order.
+Status run(int device, const TableImage* tables, size_t count, Op op, std::vector<uint8_t>* ok_out,
+           size_t* nbad_out) {
+  Plan plan;
+  make_plan(tables, count, &plan);
+  if (plan.chunks.empty()) return Status::OK();
+  std::vector<size_t> ok_base(count + 1, 0);
+  for (size_t t = 0; t < count; t++) ok_base[t + 1] = ok_base[t] + tables[t].n;
+  std::vector<uint8_t> pinned(count);
+  for (size_t t = 0; t < count; t++) pinned[t] = host_pinned(tables[t].file);
+
+  SessionLease s;
+  Status st = s.Open(device);
+  if (!st.ok()) return st;
+  const size_t meta_bytes = plan.max_blocks * (sizeof(BlockHandle) + 1) + 16;
+  const size_t res_bytes = plan.max_blocks * 4 + 16;
+  size_t nbad = 0;
+
+  // chunk sg.tag's results, from its stage (host side)
+  auto finish = [&](Stage& sg) -> Status {
+    const hipError_t e = s->wait(sg);
+    if (e != hipSuccess) return hip_status(e, op == Op::kSeal ? "seal" : "verify");
+    const Chunk& ch = plan.chunks[sg.tag];
+    size_t j = 0;
+    for (const Piece& pc : ch.pieces) {
+      const TableImage& tb = tables[pc.t];
+      for (size_t k = pc.first; k < pc.first + pc.count; k++, j++) {
+        const size_t b = plan.order[pc.t][k];
+        if (op == Op::kSeal) {  // [type][EncodeFixed32(masked crc)] (table_builder.cc:245-249)
+          uint32_t m;
+          memcpy(&m, sg.res.h + 4 * j, 4);
+          char* t = tb.file + tb.handles[b].offset + tb.handles[b].size;
+          t[0] = (char)tb.types[b];
+          for (int q = 0; q < 4; q++) t[1 + q] = (char)(m >> (8 * q));
+        } else {
+          const uint8_t good = sg.res.h[j];
+          if (!good) nbad++;
+          if (ok_out) (*ok_out)[ok_base[pc.t] + b] = good;
+        }
+      }
+    }
+    return Status::OK();
+  };
+
+  for (size_t c = 0; c < plan.chunks.size(); c++) {
+    Stage& sg = s->stage((int)(c % HostSession::kStages));
+    if (sg.busy) {
+      st = finish(sg);
+      if (!st.ok()) return st;
+    }
+    const Chunk& ch = plan.chunks[c];
+    hipError_t e = sg.bulk.reserve(std::max<size_t>(HostSession::kChunkBytes, ch.bytes));
+    if (e == hipSuccess) e = sg.meta.reserve(meta_bytes);
+    if (e == hipSuccess) e = sg.res.reserve(res_bytes);
+    if (e != hipSuccess) return hip_status(e, "staging buffers");
+    // per-block inputs: handles rebased into the chunk, then the types
+    BlockHandle* hh = reinterpret_cast<BlockHandle*>(sg.meta.h);
+    uint8_t* ty = sg.meta.h + ch.blocks * sizeof(BlockHandle);
+    size_t j = 0;
+    bool direct = true;
+    for (const Piece& pc : ch.pieces) {
+      const TableImage& tb = tables[pc.t];
+      for (size_t k = pc.first; k < pc.first + pc.count; k++, j++) {
+        const size_t b = plan.order[pc.t][k];
+        hh[j] = BlockHandle{tb.handles[b].offset - pc.lo + pc.dst, tb.handles[b].size};
+        if (op == Op::kSeal) ty[j] = tb.types[b];
+      }
+      direct = direct && pinned[pc.t];
+    }
+    // the bytes: DMA straight from page-locked images, else via the stage's pinned buffer
+    if (direct) {
+      for (const Piece& pc : ch.pieces)
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(sg.bulk.d + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo,
+                             hipMemcpyHostToDevice, sg.stream);
+    } else {
+      for (const Piece& pc : ch.pieces)
+        parallel_copy(sg.bulk.h + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo);
+      e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, ch.bytes, hipMemcpyHostToDevice, sg.stream);
+    }
+    const size_t meta_n = ch.blocks * sizeof(BlockHandle) + (op == Op::kSeal ? ch.blocks : 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "H2D");
+    const uint64_t* d_h = reinterpret_cast<const uint64_t*>(sg.meta.d);
+    int rc;
+    if (op == Op::kSeal)
+      rc = lsbm_sst_trailer_crcs_dev(sg.bulk.d, ch.bytes, d_h, sg.meta.d + ch.blocks * sizeof(BlockHandle),
+                                     ch.blocks, reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream);
+    else
+      rc = lsbm_sst_verify_dev(sg.bulk.d, ch.bytes, d_h, ch.blocks, sg.res.d, nullptr, sg.stream);
+    if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+    e = hipMemcpyAsync(sg.res.h, sg.res.d, ch.blocks * (op == Op::kSeal ? 4 : 1),
+                       hipMemcpyDeviceToHost, sg.stream);
+    if (e == hipSuccess) e = hipEventRecord(sg.done, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "D2H");
+    sg.busy = true;
+    sg.tag = c;
+  }
+  // the remaining stages, oldest chunk first
+  for (size_t c = plan.chunks.size() > (size_t)HostSession::kStages
+                      ? plan.chunks.size() - HostSession::kStages : 0;
+       c < plan.chunks.size(); c++) {
+    Stage& sg = s->stage((int)(c % HostSession::kStages));
+    if (sg.busy) {
+      st = finish(sg);
+      if (!st.ok()) return st;
+    }
+  }
+  if (nbad_out) *nbad_out = nbad;
+  return Status::OK();
 }
 
 }  // namespace
+
+Status SealTables(int device, const TableImage* tables, size_t count) {
+  for (size_t t = 0; t < count; t++) {
+    const TableImage& tb = tables[t];
+    if (tb.n == 0) continue;
+    if (!tb.file || !tb.handles || !tb.types) return Status::InvalidArgument("null pointer");
+    Status s = check_handles(tb.file_size, tb.handles, tb.n);
+    if (!s.ok()) return s;
+  }
+  return run(device, tables, count, Op::kSeal, nullptr, nullptr);
+}
+
+Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok) {
+  size_t total = 0;
+  for (size_t t = 0; t < count; t++) total += tables[t].n;
+  if (ok) ok->assign(total, 1);
+  for (size_t t = 0; t < count; t++) {
+    const TableImage& tb = tables[t];
+    if (tb.n == 0) continue;
+    if (!tb.file || !tb.handles) return Status::InvalidArgument("null pointer");
+    Status s = check_handles(tb.file_size, tb.handles, tb.n);
+    if (!s.ok()) return s;
+  }
+  size_t nbad = 0;
+  Status s = run(device, tables, count, Op::kVerify, ok, &nbad);
+  if (!s.ok()) return s;
+  return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
+}
 
 Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
                   const uint8_t* types, size_t n) {
   if (n == 0) return Status::OK();
   if (!file || !handles || !types) return Status::InvalidArgument("null pointer");
-  Status s = check_handles(file_size, handles, n);
-  if (!s.ok()) return s;
-  DeviceBuffers d;
-  s = stage(device, file, file_size, handles, n, types, &d);
-  if (!s.ok()) return s;
-  if (lsbm_sst_seal_dev(d.file, file_size, d.handles, d.aux, n, nullptr, d.stream.get()) != LSBM_OK)
-    return Status::IOError(lsbm_crc32c_last_error());
-  // Bring the image back whole through the pinned bounce: one streamed copy
-  // instead of one 5-byte hipMemcpyAsync (a runtime call) per block.  The
-  // device image is the host image plus the trailers.
-  const hipError_t e = d.bounce.to_host(file, d.file, file_size, d.stream.get());
-  if (e != hipSuccess) return hip_status(e, "seal");
-  return Status::OK();
+  const TableImage t{file, file_size, handles, types, n};
+  return SealTables(device, &t, 1);
 }
 
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
@@ -98,18 +270,8 @@ Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockH
   if (ok) ok->assign(n, 1);
   if (n == 0) return Status::OK();
   if (!file || !handles) return Status::InvalidArgument("null pointer");
-  Status s = check_handles(file_size, handles, n);
-  if (!s.ok()) return s;
-  DeviceBuffers d;
-  s = stage(device, file, file_size, handles, n, nullptr, &d);
-  if (!s.ok()) return s;
-  if (lsbm_sst_verify_dev(d.file, file_size, d.handles, n, d.aux, d.nbad, d.stream.get()) != LSBM_OK)
-    return Status::IOError(lsbm_crc32c_last_error());
-  uint32_t nbad = 0;
-  hipError_t e = d.bounce.to_host(&nbad, d.nbad, sizeof(nbad), d.stream.get());
-  if (e == hipSuccess && ok) e = d.bounce.to_host(ok->data(), d.aux, n, d.stream.get());
-  if (e != hipSuccess) return hip_status(e, "verify");
-  return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
+  const TableImage t{const_cast<char*>(file), file_size, handles, nullptr, n};
+  return VerifyTables(device, &t, 1, ok);
 }
 
 }  // namespace lsbm

@@ -5,10 +5,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <random>
 #include <set>
 #include <string>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "lsbm/table_checksum.h"
 #include "util/crc32c.h"
@@ -76,7 +79,56 @@ int main() {
   lsbm::BlockHandle trunc{file_size - 3, 10};
   s = lsbm::VerifyBlocks(0, file.data(), file.size(), &trunc, 1, &ok);
   EXPECT(s.IsCorruption() && s.ToString() == "Corruption: truncated block read");
-  printf("%s (%zu blocks, %llu bytes)\n", fails ? "FAILED" : "OK", n,
-         (unsigned long long)file_size);
+
+  // ---- SealTables / VerifyTables: many tables, one pipeline ----
+  // 40 tables of 0..~6 MiB (some empty, one with its handles out of order,
+  // one page-locked) sealed at once; every trailer checked against the
+  // per-block reference pattern, then verify with one corrupted block.
+  const size_t nt = 40;
+  std::vector<std::string> files(nt);
+  std::vector<std::vector<lsbm::BlockHandle>> hs(nt);
+  std::vector<std::vector<uint8_t>> tys(nt);
+  std::vector<lsbm::TableImage> im(nt);
+  for (size_t t = 0; t < nt; t++) {
+    const size_t nb = t == 3 ? 0 : (rng() % 1500);
+    std::vector<uint64_t> sz(nb);
+    for (auto& x : sz) x = rng() % 3 == 0 ? rng() % 200 : 3000 + rng() % 3000;
+    uint64_t fs = 0;
+    hs[t] = lsbm::LayoutBlocks(sz, &fs);
+    files[t].assign(fs + 7, '\0');
+    for (auto& c : files[t]) c = (char)(' ' + rng() % 95);
+    tys[t].resize(nb);
+    for (auto& y : tys[t]) y = rng() & 1;
+    if (t == 5) std::reverse(hs[t].begin(), hs[t].end());  // handles out of offset order
+    im[t] = lsbm::TableImage{&files[t][0], files[t].size(), hs[t].data(), tys[t].data(), nb};
+  }
+  // table 7 page-locked: its chunks are DMA-ed from the image itself
+  const bool reg = hipHostRegister(&files[7][0], files[7].size(), hipHostRegisterDefault) == hipSuccess;
+  EXPECT(reg);
+  lsbm::Status st = lsbm::SealTables(0, im.data(), nt);
+  EXPECT(st.ok());
+  size_t checked = 0;
+  for (size_t t = 0; t < nt; t++)
+    for (size_t i = 0; i < hs[t].size(); i++, checked++) {
+      const char* block = files[t].data() + hs[t][i].offset;
+      char trailer[5];
+      trailer[0] = (char)tys[t][i];
+      uint32_t crc = leveldb::crc32c::Extend(leveldb::crc32c::Value(block, hs[t][i].size), trailer, 1);
+      encode_fixed32(trailer + 1, leveldb::crc32c::Mask(crc));
+      EXPECT(memcmp(trailer, block + hs[t][i].size, 5) == 0);
+    }
+  std::vector<uint8_t> oks;
+  st = lsbm::VerifyTables(0, im.data(), nt, &oks);
+  EXPECT(st.ok() && oks.size() == checked);
+  files[9][hs[9][4].offset] ^= 0x08;  // a payload byte of table 9, block 4
+  st = lsbm::VerifyTables(0, im.data(), nt, &oks);
+  EXPECT(st.IsCorruption());
+  size_t base9 = 0, nbad = 0;
+  for (size_t t = 0; t < 9; t++) base9 += hs[t].size();
+  for (size_t i = 0; i < oks.size(); i++) nbad += !oks[i];
+  EXPECT(nbad == 1 && oks[base9 + 4] == 0);
+  if (reg) (void)hipHostUnregister(&files[7][0]);
+  printf("%s (%zu blocks, %llu bytes; %zu blocks over %zu tables)\n", fails ? "FAILED" : "OK", n,
+         (unsigned long long)file_size, checked, nt);
   return fails ? 1 : 0;
 }

@@ -261,9 +261,11 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = tmp_path / "table_gpu_test"
     libdir = os.path.join(repo, "lsbm_amd")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(repo, "include"),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(repo, "include"), "-I", "/opt/rocm/include",
                     os.path.join(repo, "tests", "cpp", "table_gpu_test.cc"), "-L", libdir,
-                    "-llsbm_crc32c", "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+                    "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")
