@@ -160,6 +160,14 @@ int lsbm_crc32c_batch_host(int device, const void* h_base, const uint64_t* h_off
                            uint64_t n_blocks, const uint32_t* h_init, uint32_t* h_out,
                            uint32_t flags);
 
+/* The same over several devices: the blocks are cut into contiguous shards
+ * of about equal bytes, one per devices[k], each checksummed by its own host
+ * thread through its own device's staging and streams.  No collective and no
+ * device-to-device traffic: blocks are independent. */
+int lsbm_crc32c_batch_host_multi(const int* devices, int n_devices, const void* h_base,
+                                 const uint64_t* h_offsets, uint64_t n_blocks,
+                                 const uint32_t* h_init, uint32_t* h_out, uint32_t flags);
+
 /* ---- device helpers ----
  * d_dst[d_dst_off[i], +d_len[i]) = d_src[d_src_off[i], +d_len[i]) for i < n
  * (segments must not overlap each other's destinations): compacts

@@ -47,6 +47,7 @@ SIGNATURES = {
     "lsbm_log_verify_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_log_crcs_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_crc32c_batch_host": (_int, [_int, _vp, _vp, _u64, _vp, _vp, _u32]),
+    "lsbm_crc32c_batch_host_multi": (_int, [_vp, _int, _vp, _vp, _u64, _vp, _vp, _u32]),
     "lsbm_gather_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),
     "lsbm_stream_read_dev": (_int, [_vp, _u64, _vp, _vp]),

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -719,6 +720,54 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
   }
   hipSetDevice(prev);
   return rc;
+}
+
+// Shards one host batch over several devices: contiguous runs of blocks of
+// about equal bytes, one host thread per device, each running the
+// host-staged pipeline above on its own device.  No data moves between the
+// devices (the CRCs are independent); each writes its slice of h_out.
+__attribute__((visibility("default"))) int lsbm_crc32c_batch_host_multi(
+    const int* devices, int n_devices, const void* h_base, const uint64_t* h_offsets,
+    uint64_t n_blocks, const uint32_t* h_init, uint32_t* h_out, uint32_t flags) {
+  if (n_blocks == 0) return LSBM_OK;
+  if (!devices || n_devices <= 0 || !h_base || !h_offsets || !h_out)
+    return fail(LSBM_ERR_INVALID, "null pointer or no devices");
+  // shard boundaries by bytes (extents may be unsorted: fall back to counts)
+  std::vector<uint64_t> cut(n_devices + 1, n_blocks);
+  cut[0] = 0;
+  uint64_t total = 0;
+  bool sorted = true;
+  for (uint64_t i = 0; i < n_blocks; i++) {
+    const uint64_t s0 = h_offsets[i], s1 = h_offsets[i + 1];
+    total += s1 > s0 ? s1 - s0 : 0;
+    sorted = sorted && s1 >= s0;
+  }
+  if (sorted && total) {
+    uint64_t acc = 0;
+    int d = 1;
+    for (uint64_t i = 0; i < n_blocks && d < n_devices; i++) {
+      acc += h_offsets[i + 1] - h_offsets[i];
+      while (d < n_devices && acc * n_devices >= total * (uint64_t)d) cut[d++] = i + 1;
+    }
+  } else {
+    for (int d = 1; d < n_devices; d++) cut[d] = n_blocks * d / n_devices;
+  }
+  std::vector<int> rc(n_devices, LSBM_OK);
+  std::vector<std::string> err(n_devices);
+  std::vector<std::thread> th;
+  for (int d = 0; d < n_devices; d++) {
+    if (cut[d + 1] <= cut[d]) continue;
+    th.emplace_back([&, d] {
+      const uint64_t lo = cut[d], cnt = cut[d + 1] - cut[d];
+      rc[d] = lsbm_crc32c_batch_host(devices[d], h_base, h_offsets + lo, cnt,
+                                     h_init ? h_init + lo : nullptr, h_out + lo, flags);
+      if (rc[d] != LSBM_OK) err[d] = t_last_error;  // (per-thread error text)
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < n_devices; d++)
+    if (rc[d] != LSBM_OK) return fail(rc[d], err[d].c_str());
+  return LSBM_OK;
 }
 
 }  // extern "C"

@@ -134,6 +134,25 @@ def crc32c_batch_host(data, offsets, init=None, masked=False, device=0):
     return out
 
 
+def crc32c_batch_host_multi(data, offsets, devices, init=None, masked=False):
+    """crc32c_batch_host sharded over `devices` (one host thread per device,
+    contiguous shards of about equal bytes, no collective)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    out = np.empty(max(n, 0), dtype=np.uint32)
+    if init is not None:
+        init = np.ascontiguousarray(init, dtype=np.uint32)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    flags = LSBM_CRC32C_MASKED if masked else 0
+    check(lib().lsbm_crc32c_batch_host_multi(devs, len(devices), data.ctypes.data_as(ctypes.c_void_p),
+                                             offsets.ctypes.data_as(ctypes.c_void_p), max(n, 0),
+                                             init.ctypes.data_as(ctypes.c_void_p) if init is not None
+                                             else None, out.ctypes.data_as(ctypes.c_void_p), flags),
+          "lsbm_crc32c_batch_host_multi")
+    return out
+
+
 def fill_splitmix64(buf, seed, stream=None):
     """buf[k] = byte k of the splitmix64 stream `seed` (uint8 device tensor)."""
     _require_cuda(buf)

@@ -552,3 +552,18 @@ def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax)
     assert np.array_equal(out, want)
     ok, nb = table.verify_blocks(d[:total], dh)
     assert int(nb.item()) == 0 and bool(ok.all())
+
+
+def test_host_staged_multi_device_shards(torch_cuda, oracle):
+    """lsbm_crc32c_batch_host_multi: contiguous shards, one host thread per
+    device.  The box has one GPU, so the shards all go to device 0 through
+    concurrent threads (the engine serialises them per device); every CRC must
+    still equal the oracle's."""
+    from lsbm_amd import engine
+    starts, ends, total = _ragged_case(41, 30000, 9000)
+    offs = np.concatenate([starts, ends[-1:]]).astype(np.uint64)
+    data = stream_bytes(41, 0, total)
+    init = np.random.default_rng(1).integers(0, 2**32, size=30000, dtype=np.uint64).astype(np.uint32)
+    for devs in ([0], [0, 0], [0, 0, 0, 0]):
+        got = engine.crc32c_batch_host_multi(data, offs, devs, init=init, masked=True)
+        assert np.array_equal(got, oracle.batch_offsets(data, offs, init, masked=True)), devs

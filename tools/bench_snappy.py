@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Snappy block codec rates on one GPU, db_bench shaped:
-~4,118-B data blocks as db_bench's fill workload writes them
-(tests/golden/snappy_inputs.py dbbench_block: BlockBuilder layout, internal
-keys "user%019d", 100-byte values that compress to ~50%).  A pool of distinct
-blocks is built on the host, copied to HBM and tiled to the batch size, so
-every block of the batch sits at its own address; all input is resident in
-HBM before timing.  One JSON line per measurement:
+~4,118-B data blocks as db_bench's fill workload writes them (BlockBuilder
+layout, internal keys "user%019d", 100-byte values that compress to ~50%;
+tools/dbbench_blocks.c, the layout of tests/golden/snappy_inputs.py
+dbbench_block).  Every block of the batch is distinct (262,144 blocks, 1.08 GB
+by default), built on the host and copied to HBM before timing.  One JSON line
+per measurement:
 
   snappy_compress    lsbm_snappy_compress_dev over the batch (WriteBlock's
                      RawCompress, table/table_builder.cc:186)
@@ -15,7 +15,9 @@ HBM before timing.  One JSON line per measurement:
 value = uncompressed GB/s (raw bytes / kernel time).  The roofline uses the
 algorithmic HBM bytes per block: raw + compressed (read one, write the other).
 cpu_baseline: libsnappy itself (the pyarrow build the oracle is pinned to) on
-one host core over a bounded sample, plus the oracle's C restatement.
+every usable host core (one process per core, each over its own share of the
+same blocks, started together), with the one-core rate beside it, plus the
+oracle's C restatement on one core.
 """
 import argparse
 import ctypes
@@ -48,47 +50,97 @@ def timed(torch, fn, reps, warm=2):
     return e0.elapsed_time(e1) / 1e3 / reps
 
 
-def pool_blocks(n_pool):
-    from snappy_inputs import dbbench_block
-    blocks, k = [], 0
-    for i in range(n_pool):
-        b, k = dbbench_block(900000 + i, k)
-        blocks.append(b)
-    return blocks
+def make_blocks(n, seed=7):
+    """n distinct db_bench-shaped blocks: (bytes as np.uint8, offsets[n+1])."""
+    import subprocess
+    so = os.path.join(REPO, "build", "libdbgen.so")
+    if not os.path.exists(so):
+        os.makedirs(os.path.dirname(so), exist_ok=True)
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", so,
+                        os.path.join(HERE, "dbbench_blocks.c")], check=True)
+    lib = ctypes.CDLL(so)
+    lib.dbgen_blocks.restype = ctypes.c_size_t
+    lib.dbgen_blocks.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                 ctypes.c_void_p]
+    need = lib.dbgen_blocks(seed, n, None, 0, None)
+    buf = np.empty(need, np.uint8)
+    offs = np.empty(n + 1, np.uint64)
+    lib.dbgen_blocks(seed, n, buf.ctypes.data, need, offs.ctypes.data)
+    return buf, offs
 
 
-def cpu_baselines(blocks, seconds=10.0):
-    """(libsnappy compress, libsnappy uncompress, oracle compress) in raw GB/s
-    on one core, each over repeated passes of `blocks` for ~seconds/3."""
+def usable_cores():
+    sys.path.insert(0, REPO)
+    from bench import usable_cores as uc
+    return uc()[0]
+
+
+_BLOCKS = None  # (buf, offs, compressed list) shared with forked workers
+
+
+def _worker(args):
+    """One process: libsnappy over blocks [lo, hi) for ~seconds; raw bytes/s."""
+    kind, lo, hi, seconds, barrier = args
+    import pyarrow as pa
+    codec = pa.Codec("snappy")
+    buf, offs, comp = _BLOCKS
+    blocks = [buf[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(lo, hi)]
+    raw = sum(len(b) for b in blocks)
+    barrier.wait()
+    t0, passes = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        if kind == "compress":
+            for b in blocks:
+                codec.compress(b, asbytes=True)
+        else:
+            for c, b in zip(comp[lo:hi], blocks):
+                codec.decompress(c, decompressed_size=len(b), asbytes=True)
+        passes += 1
+    return raw * passes, time.perf_counter() - t0
+
+
+def cpu_baselines(buf, offs, n_sample, seconds=4.0):
+    """libsnappy (pyarrow) compress / uncompress over the first n_sample
+    blocks: one core, and all usable cores (one forked process per core, each
+    over its own share of the sample, started together).  Raw GB/s."""
+    global _BLOCKS
+    import multiprocessing as mp
     out = {}
     try:
         import pyarrow as pa
-        codec = pa.Codec("snappy")
-        comp = [codec.compress(b, asbytes=True) for b in blocks]
-        raw = sum(len(b) for b in blocks)
-        for name, fn in (("compress", lambda: [codec.compress(b, asbytes=True) for b in blocks]),
-                         ("uncompress", lambda: [codec.decompress(c, decompressed_size=len(b), asbytes=True)
-                                                 for c, b in zip(comp, blocks)])):
-            t0, passes = time.perf_counter(), 0
-            while time.perf_counter() - t0 < seconds / 3:
-                fn()
-                passes += 1
-            out["libsnappy_" + name] = raw * passes / (time.perf_counter() - t0) / 1e9
     except ImportError:
-        pass
+        return out
+    codec = pa.Codec("snappy")
+    comp = [codec.compress(buf[int(offs[i]):int(offs[i + 1])].tobytes(), asbytes=True)
+            for i in range(n_sample)]
+    _BLOCKS = (buf, offs, comp)
+    cores = usable_cores()
+    ctx = mp.get_context("fork")
+    for kind in ("compress", "uncompress"):
+        for nproc in (1, cores):
+            with ctx.Manager() as m:
+                bar = m.Barrier(nproc)
+                cut = [n_sample * k // nproc for k in range(nproc + 1)]
+                with ctx.Pool(nproc) as pool:
+                    res = pool.map(_worker, [(kind, cut[k], cut[k + 1], seconds, bar)
+                                             for k in range(nproc)])
+            rate = sum(b for b, _ in res) / max(t for _, t in res) / 1e9
+            out[f"libsnappy_{kind}_{'1core' if nproc == 1 else 'all'}"] = rate
+    out["cores"] = cores
     lib = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle_snappy.so"))
-    data = np.frombuffer(b"".join(blocks), np.uint8)
-    offs = np.zeros(len(blocks) + 1, np.uint64)
-    offs[1:] = np.cumsum([len(b) for b in blocks])
-    caps = np.array([32 + len(b) + len(b) // 6 for b in blocks], np.uint64)
-    oo = np.zeros(len(blocks) + 1, np.uint64)
+    m = min(n_sample, 2048)
+    data = np.ascontiguousarray(buf[:int(offs[m])])
+    o = np.ascontiguousarray(offs[:m + 1])
+    lens = np.diff(o)
+    caps = (32 + lens + lens // 6).astype(np.uint64)
+    oo = np.zeros(m + 1, np.uint64)
     oo[1:] = np.cumsum(caps)
     cout = np.zeros(int(oo[-1]), np.uint8)
-    osz = np.zeros(len(blocks), np.uint64)
+    osz = np.zeros(m, np.uint64)
     t0, passes = time.perf_counter(), 0
-    while time.perf_counter() - t0 < seconds / 3:
-        lib.so_compress_batch(ctypes.c_void_p(data.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
-                              ctypes.c_uint64(len(blocks)), ctypes.c_void_p(cout.ctypes.data),
+    while time.perf_counter() - t0 < seconds / 2:
+        lib.so_compress_batch(ctypes.c_void_p(data.ctypes.data), ctypes.c_void_p(o.ctypes.data),
+                              ctypes.c_uint64(m), ctypes.c_void_p(cout.ctypes.data),
                               ctypes.c_void_p(oo.ctypes.data), ctypes.c_void_p(osz.ctypes.data))
         passes += 1
     out["oracle_compress"] = data.size * passes / (time.perf_counter() - t0) / 1e9
@@ -98,24 +150,22 @@ def cpu_baselines(blocks, seconds=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=262144)
-    ap.add_argument("--pool", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--cpu-seconds", type=float, default=9.0)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--cpu-sample", type=int, default=65536)
     args = ap.parse_args()
 
+    buf, offs_h = make_blocks(args.blocks)
+    n = args.blocks
+    # the CPU baseline first, in forked worker processes, before this process
+    # touches the GPU (no child ever holds a device context)
+    cpu = cpu_baselines(buf, offs_h, min(n, args.cpu_sample), args.cpu_seconds)
     import torch
     from lsbm_amd import engine, snappy
     engine.init(0)
-    blocks = pool_blocks(args.pool)
-    lens = np.array([len(b) for b in blocks], np.int64)
-    pool = torch.from_numpy(np.frombuffer(b"".join(blocks), np.uint8).copy()).cuda()
-    reps = (args.blocks + args.pool - 1) // args.pool
-    n = reps * args.pool
-    data = pool.repeat(reps)
-    all_lens = torch.from_numpy(np.tile(lens, reps)).cuda()
-    offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
-    torch.cumsum(all_lens, 0, out=offs[1:])
-    raw_bytes = int(offs[-1].item())
+    data = torch.from_numpy(buf).cuda()
+    offs = torch.from_numpy(offs_h.astype(np.int64)).cuda()
+    raw_bytes = int(offs_h[-1])
 
     out, oo, ol = snappy.compress(data, offs)
     t_c = timed(torch, lambda: snappy.compress(data, offs, out=out, out_offsets=oo, out_len=ol), args.reps)
@@ -127,7 +177,7 @@ def main():
     oo_h, ol_h, out_h = oo.cpu().numpy(), ol.cpu().numpy(), None
     mism = 0
     for i in range(0, n, max(1, n // 512)):
-        b = blocks[i % args.pool]
+        b = buf[int(offs_h[i]):int(offs_h[i + 1])].tobytes()
         s = int(oo_h[i])
         g = out[s:s + int(ol_h[i])].cpu().numpy().tobytes()
         mism += g != orc.compress(b)
@@ -143,15 +193,14 @@ def main():
     nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
     snappy.uncompress(cdata, coffs, out=uout, out_offsets=uo, ok=ok, n_bad=nbad)
     torch.cuda.synchronize()
-    rt_ok = bool(torch.equal(uout, data[:raw_bytes])) and int(nbad.item()) == 0
+    rt_ok = bool(torch.equal(uout, data)) and int(nbad.item()) == 0
     nbad.zero_()
     t_u = timed(torch, lambda: snappy.uncompress(cdata, coffs, out=uout, out_offsets=uo, ok=ok,
                                                  n_bad=nbad), args.reps)
 
-    cpu = cpu_baselines(blocks[:1024], args.cpu_seconds)
     alg = raw_bytes + comp_bytes
     common = {"unit": "GB/s", "higher_is_better": True, "n_gpus": 1, "dtype": "u8",
-              "data": "synthetic db_bench-shaped data blocks (%d distinct, tiled), resident in HBM" % args.pool,
+              "data": "synthetic db_bench-shaped data blocks, %d distinct, resident in HBM" % n,
               "config": {"workload": "%d x ~%d B SSTable data blocks" % (n, raw_bytes // n),
                          "blocks": n, "raw_bytes": raw_bytes, "compressed_bytes": comp_bytes,
                          "ratio": round(comp_bytes / raw_bytes, 4)}}
@@ -163,15 +212,18 @@ def main():
                             "frac": round(alg / t / 1e9 / HBM, 4), "traffic": None,
                             "note": "algorithmic bytes = raw + compressed per block; the kernels are "
                                     "latency bound (serial tag walk), see DESIGN.md section 11"}
-        if base in cpu:
-            line["cpu_baseline"] = {"value": round(cpu[base], 3), "unit": "GB/s", "cores": 1,
+        if base + "_all" in cpu:
+            line["cpu_baseline"] = {"value": round(cpu[base + "_all"], 3), "unit": "GB/s",
+                                    "cores": cpu["cores"],
                                     "kind": "libsnappy (pyarrow %s build, the library the oracle is pinned to)"
                                             % __import__("pyarrow").__version__,
-                                    "sample": "1024 distinct blocks, repeated ~%.0f s" % (args.cpu_seconds / 3)}
-            line["vs_cpu_core"] = round(raw_bytes / t / 1e9 / cpu[base], 1)
+                                    "sample": "%d distinct blocks, one process per usable core, ~%.0f s"
+                                              % (min(n, args.cpu_sample), args.cpu_seconds),
+                                    "single_core": round(cpu[base + "_1core"], 3)}
+            line["vs_cpu_all_cores"] = round(raw_bytes / t / 1e9 / cpu[base + "_all"], 2)
         if name == "snappy_compress":
             line["sample_mismatches"] = int(mism)
-            line["oracle_compress_1core_GBps"] = round(cpu["oracle_compress"], 3)
+            line["oracle_compress_1core_GBps"] = round(cpu.get("oracle_compress", 0), 3)
         else:
             line["roundtrip_ok"] = rt_ok
         print(json.dumps(line), flush=True)
