@@ -372,6 +372,71 @@ __device__ __forceinline__ uint32_t unaligned_word(uint32_t lo, uint32_t hi, uin
   return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)addr & 3u);
 }
 
+// Start offset of block b in [0, n]: offsets[b]; a handle's offset, and the
+// end of the last block for b = n.  Monotone for a sorted batch.
+template <uint32_t kExt>
+__device__ __forceinline__ uint64_t start_key(const RaggedArgs& a, uint64_t b) {
+  if constexpr (kExt == kExtOffsets) {
+    return reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.offsets))[b];
+  } else {
+    const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
+    const uint64_t i = b < a.n ? b : a.n - 1;
+    const uint64_t x = h[2 * i];
+    return b < a.n ? x : x + h[2 * i + 1];
+  }
+}
+
+// Byte-balanced wave ranges.  With block lengths drawn from a skewed
+// distribution, equal block COUNTS per wave leave the heaviest wave ~9% above
+// the mean (10M Zipf blocks over 4,096 waves), and the kernel waits for it.
+// Wave w's range is [f(w), f(w + 1)) with f(w) the first block whose start is
+// at or past key(0) + (key(n) - key(0)) w / nwaves.  Both ends are found
+// together, lanes 0-31 for f(w) and 32-63 for f(w + 1), by a 32-ary search
+// (one load per lane per step, ~5 steps for 10M blocks).  The search only
+// ever compares key(p) >= t, so its result is non-decreasing in t for ANY
+// key array: the ranges tile [0, n) exactly even for an unsorted batch (which
+// is then merely not balanced).
+template <uint32_t kExt>
+__device__ __forceinline__ void byte_ranges(const RaggedArgs& a, uint64_t wave, uint64_t nwaves,
+                                            uint64_t& b_lo, uint64_t& b_hi) {
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, k = lane & 31u;
+  const uint64_t k0 = start_key<kExt>(a, 0), kn = start_key<kExt>(a, a.n);
+  if (kn <= k0) return;  // (wave-uniform) keep the equal counts
+  const uint64_t w = wave + half;
+  const uint64_t t = k0 + (kn - k0) * w / nwaves;  // (kn - k0 < 2^50 bytes)
+  // the answer lies in [lo, hi]; hi when no key in [lo, hi) reaches t.
+  // f(0) = 0 and f(nwaves) = n.
+  uint64_t lo = w >= nwaves ? a.n : 0, hi = w == 0 ? 0 : a.n;
+  for (;;) {
+    if (__ballot(hi - lo > 32u) == 0ull) break;
+    const uint64_t step = (hi - lo + 31u) >> 5;
+    uint64_t p = lo + (k + 1) * step - 1u;
+    p = hi > lo ? (p < hi ? p : hi - 1u) : 0u;  // every load in [0, n]
+    const bool ge = hi > lo && start_key<kExt>(a, p) >= t;
+    const uint32_t m = (uint32_t)(__ballot(ge) >> (32u * half));
+    if (hi - lo > 32u) {
+      if (m == 0u) {
+        lo = hi;
+      } else {
+        const uint32_t ks = (uint32_t)__builtin_ctz(m);
+        const uint64_t pk = (uint64_t)__shfl((unsigned long long)p, (int)(32u * half + ks));
+        lo = lo + ks * step;
+        hi = pk;
+      }
+    }
+  }
+  const uint64_t q = lo + k < hi ? lo + k : 0u;
+  const bool ge = lo + k < hi && start_key<kExt>(a, q) >= t;
+  const uint32_t m = (uint32_t)(__ballot(ge) >> (32u * half));
+  const uint64_t f = m ? lo + (uint32_t)__builtin_ctz(m) : hi;
+  auto read64 = [](uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+  };
+  b_lo = read64(f, 0);
+  b_hi = read64(f, 32);
+}
+
 // Units kernel.  Each wave owns a contiguous range of blocks and walks it in
 // rounds of 8 units (one per lane group).  The loop is software-pipelined so
 // that no global-memory latency is exposed between rounds:
@@ -399,8 +464,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
-  // this wave's contiguous range of blocks
-  const uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
+  // this wave's contiguous range of blocks: equal counts, or equal bytes for
+  // general batches (whose lengths may be skewed; SSTable blocks and log
+  // records are near-uniform)
+  uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
+#ifndef LSBM_NO_BALANCE  // A/B builds only
+  if constexpr ((kMode == kModeOut || kMode == kModeVerify) &&
+                (kExt == kExtOffsets || kExt == kExtHandles))
+    if (args.n >= 16u * nwaves) byte_ranges<kExt>(args, wave, nwaves, b_lo, b_hi);
+#endif
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const uint32_t* __restrict__ init = args.init;
   constexpr uint32_t mode = kMode;

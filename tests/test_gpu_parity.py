@@ -126,6 +126,73 @@ def test_ragged_matches_fixed_on_same_blocks(torch_cuda):
     assert torch.equal(a, b)
 
 
+def _skewed_offsets(seed, n, base=5):
+    """Mostly 0-600-B blocks, 1% of 10-100 KB: equal block counts per wave
+    would leave some waves with several times the mean bytes."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 600, size=n)
+    big = rng.random(n) < 0.01
+    lens[big] = rng.integers(10_000, 100_000, size=int(big.sum()))
+    return (np.concatenate([[0], np.cumsum(lens)]) + base).astype(np.int64)
+
+
+@pytest.mark.parametrize("kind", ["offsets", "extents", "verify"])
+def test_ragged_byte_balanced_ranges_skewed(torch_cuda, oracle, kind):
+    """>= 16 blocks per wave: general batches cut the waves' ranges by bytes
+    (a 32-ary search over the block starts, crc32c_kernels.hip byte_ranges);
+    every block is computed exactly once whatever the cut."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n = 300_000
+    offs = _skewed_offsets(21, n)
+    data = stream_bytes(21, 0, int(offs[-1]) + 64)
+    want = oracle.batch_offsets(data, offs.astype(np.uint64), None, kind == "verify")
+    d = _dev(torch, data)
+    if kind == "offsets":
+        got = _u32(engine.crc32c_batch(d, _dev(torch, offs)))
+    elif kind == "extents":
+        ext = np.stack([offs[:-1], offs[1:] - offs[:-1]], 1).reshape(-1)
+        got = _u32(engine.crc32c_extents(d, _dev(torch, ext)))
+    else:
+        exp = want.copy()
+        flip = np.random.default_rng(5).choice(n, size=97, replace=False)
+        exp[flip] ^= 0x10
+        ok, nbad = engine.crc32c_verify(d, _dev(torch, offs), _dev(torch, exp, torch.int32),
+                                        masked=True)
+        assert int(nbad.item()) == 97  # each block checked exactly once
+        assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(flip.tolist())
+        return
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("order", ["random", "descending"])
+def test_ragged_unsorted_starts_tile_exactly(torch_cuda, oracle, order):
+    """The byte cut on a batch whose starts are not sorted: the search is
+    monotone in its target for any array, so the ranges still tile [0, n)
+    (no block twice: verify's failure count is exact)."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n = 100_000
+    rng = np.random.default_rng(17)
+    if order == "random":  # starts jitter around a rising line: e < s (empty) in ~1/4
+        offs = np.arange(n + 1, dtype=np.int64) * 30 + rng.integers(0, 400, size=n + 1)
+    else:  # every block empty but the last; key(n) > key(0), the search runs over a reversed array
+        offs = (n - np.arange(n + 1, dtype=np.int64)) * 30
+        offs[n] = offs[0] + 1
+    data = stream_bytes(17, 0, int(offs.max()) + 16)
+    want = np.empty(n, dtype=np.uint32)
+    for i in range(n):
+        s, e = int(offs[i]), int(offs[i + 1])
+        want[i] = oracle.value(data[s:max(s, e)].tobytes())
+    exp = want.copy()
+    flip = rng.choice(n, size=41, replace=False)
+    exp[flip] ^= 1
+    ok, nbad = engine.crc32c_verify(_dev(torch, data), _dev(torch, offs),
+                                    _dev(torch, exp, torch.int32))
+    assert int(nbad.item()) == 41
+    assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(flip.tolist())
+
+
 # ---------------------------------------------------------------- verify
 def test_verify_detects_single_byte_flips(torch_cuda, oracle):
     torch = torch_cuda
