@@ -17,6 +17,8 @@ namespace lsbm {
 // launchers (bloom_kernels.hip)
 hipError_t launch_bloom_build(const BloomBuildArgs& a, int grid, hipStream_t stream);
 hipError_t launch_bloom_probe(const BloomProbeArgs& a, int grid, hipStream_t stream);
+int bloom_build_blocks_per_cu();
+int bloom_probe_blocks_per_cu();
 
 namespace {
 
@@ -49,9 +51,9 @@ int probe(const uint8_t* base, const uint64_t* handles, const uint64_t* data_off
   a.k_use = lsbm_bloom_k_probe(bits_per_key, bloom_bits_use);
   a.strip = strip;
   a.mode = mode;
-  // grid-stride: no more workgroups than are resident at once (98 VGPRs ->
-  // 4 waves per SIMD = 4 workgroups of 256 per CU; hipcc -Rpass-analysis)
-  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, 4), static_cast<hipStream_t>(stream));
+  // grid-stride: no more workgroups than are resident at once
+  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, bloom_probe_blocks_per_cu()),
+                                          static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_probe_kernel");
 }
 
@@ -83,11 +85,10 @@ __attribute__((visibility("default"))) int lsbm_bloom_build_dev(
   a.bits_per_key = (uint64_t)bits_per_key;
   a.strip = strip;
   a.k = lsbm_bloom_k(bits_per_key);
-  // one wave per group of kBloomGroup filters; grid-stride with no more
-  // workgroups than are resident at once (106 SGPRs -> 6 workgroups of 256 per
-  // CU, MI355X_MICROARCH.md "Residency"; hipcc -Rpass-analysis)
+  // one wave per range of filters (groups of kBloomGroup); no more
+  // workgroups than are resident at once
   const uint64_t groups = (n_filters + kBloomGroup - 1) / kBloomGroup;
-  const hipError_t e = launch_bloom_build(a, grid_for(cus, groups, kBloomWaves, 6),
+  const hipError_t e = launch_bloom_build(a, grid_for(cus, groups, kBloomWaves, bloom_build_blocks_per_cu()),
                                           static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_build_kernel");
 }

@@ -28,6 +28,8 @@ typedef const __attribute__((address_space(1))) uint32_t* gcu32;
 typedef const __attribute__((address_space(1))) uint8_t* gcu8;
 typedef __attribute__((address_space(1))) uint32_t* gu32;
 typedef __attribute__((address_space(1))) uint8_t* gu8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gcu32x4;
 
 constexpr uint32_t kHashM = 0xc6a4a793u;     // util/hash.cc:20
 constexpr uint32_t kBloomSeed = 0xbc9f1d34u;  // util/bloom.cc:14
@@ -102,6 +104,86 @@ __device__ uint32_t hash_key_batched(uint64_t s, uint64_t n, uint32_t seed) {
         h ^= h >> 24;
       }
     }
+  }
+  return h;
+}
+
+// The same hash over a key staged in LDS: byte `rel` of the wave's staging
+// area `stg` (words past the key may be read; they only feed bytes the tail
+// step drops).  One address, immediate word offsets, no clamps.
+__device__ __forceinline__ uint32_t hash_key_lds(const uint32_t* stg, uint32_t rel, uint32_t n,
+                                                 uint32_t seed) {
+  uint32_t h = seed ^ (n * kHashM);
+  if (n == 0) return h;
+  const uint32_t sh = rel & 3u;
+  const uint32_t* w0 = stg + (rel >> 2);
+  const uint32_t full = n >> 2, r = n & 3u, steps = full + (r ? 1u : 0u);
+  for (uint32_t c = 0; c < steps; c += 8) {
+    uint32_t w[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) w[j] = w0[c + j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t t = c + j;
+      const uint32_t x = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+      if (t < full) {
+        h += x;
+        h *= kHashM;
+        h ^= h >> 16;
+      } else if (t == full && r) {
+        if (r == 3) h += sext8(x >> 16) << 16;
+        if (r >= 2) h += sext8(x >> 8) << 8;
+        h += sext8(x);
+        h *= kHashM;
+        h ^= h >> 24;
+      }
+    }
+  }
+  return h;
+}
+
+// hash_key_lds when every lane of the wave hashes a key of the same length
+// nu (wave-uniform: db_bench keys are all 23 B): the step structure is then
+// scalar, straight-line code without per-step lane masks.
+__device__ __forceinline__ uint32_t hash_key_lds_uniform(const uint32_t* stg, uint32_t rel,
+                                                         uint32_t nu, uint32_t seed) {
+  uint32_t h = seed ^ (nu * kHashM);
+  if (nu == 0) return h;
+  const uint32_t sh = rel & 3u;
+  const uint32_t* w = stg + (rel >> 2);
+  const uint32_t full = nu >> 2, r = nu & 3u;
+  uint32_t lo = w[0];
+  uint32_t t = 0;
+  for (; t + 4 <= full; t += 4) {  // 16 key bytes per pass
+    const uint32_t w1 = w[t + 1], w2 = w[t + 2], w3 = w[t + 3], w4 = w[t + 4];
+    h += __builtin_amdgcn_alignbyte(w1, lo, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    h += __builtin_amdgcn_alignbyte(w2, w1, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    h += __builtin_amdgcn_alignbyte(w3, w2, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    h += __builtin_amdgcn_alignbyte(w4, w3, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    lo = w4;
+  }
+  for (; t < full; t++) {
+    const uint32_t hi = w[t + 1];
+    h += __builtin_amdgcn_alignbyte(hi, lo, sh);
+    h *= kHashM;
+    h ^= h >> 16;
+    lo = hi;
+  }
+  if (r) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(w[t + 1], lo, sh);
+    if (r == 3) h += sext8(x >> 16) << 16;
+    if (r >= 2) h += sext8(x >> 8) << 8;
+    h += sext8(x);
+    h *= kHashM;
+    h ^= h >> 24;
   }
   return h;
 }
@@ -195,6 +277,51 @@ __device__ __forceinline__ void store_window(uint64_t d, const uint32_t* bm, uin
     *reinterpret_cast<gu32>(d + head + 4ull * i) = __builtin_amdgcn_alignbyte(bm[i + 1], bm[i], head);
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The bloom hash of this lane's key [s, s + n) (n = 0 on inactive lanes), for
+// a whole wave.  When the wave's non-empty keys all lie inside one span that
+// fits `avail` bytes of the wave's LDS staging area (64 db_bench keys: 64 x
+// 31 B), the span is staged with coalesced 16-B loads -- only 16-B chunks
+// that overlap the keys, so never a page the keys do not touch -- and hashed
+// from LDS (scalar step structure when all keys have one length); else every
+// lane reads its own key's words from global memory.
+__device__ __forceinline__ uint32_t wave_hash(uint32_t* stg, uint32_t avail, uint64_t s, uint64_t n,
+                                              bool act) {
+  const uint32_t lane = threadIdx.x & 63u;
+  // the span from the first to the last non-empty key (an empty key's
+  // start need not be a readable address)
+  const uint64_t nz = __ballot(n > 0);
+  const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
+  const uint32_t ll = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
+  const uint64_t lo = readlane64(s, fl), hi = readlane64(s + n, ll);
+  const uint64_t sbase = lo & ~15ull;
+  const bool inside = n == 0 || (s >= lo && s + n <= hi);
+  const bool staged = nz != 0 && hi > lo && hi - sbase <= avail && __ballot(!inside) == 0ull;
+  if (!staged) return hash_key_batched(s, n, kBloomSeed);
+  const uint32_t nch = (uint32_t)((hi - sbase + 15) >> 4);
+  for (uint32_t c = lane; c < nch; c += 64)
+    *reinterpret_cast<u32x4*>(stg + 4 * c) = *reinterpret_cast<gcu32x4>(sbase + 16ull * c);
+  wave_phase();
+  const uint32_t rel = act ? (uint32_t)(s - sbase) : 0u;
+  const uint32_t n0 = (uint32_t)readlane64(n, fl);
+  uint32_t h;
+#ifdef LSBM_NO_UNIFORM_HASH  // A/B builds only
+  if (false)
+#else
+  if (__ballot(act && n != n0) == 0ull)  // (inactive lanes' hashes are dropped)
+#endif
+    h = hash_key_lds_uniform(stg, rel, __builtin_amdgcn_readfirstlane(n0), kBloomSeed);
+  else
+    h = hash_key_lds(stg, rel, (uint32_t)n, kBloomSeed);
+  wave_phase();  // (the next staging writes after these reads)
+  return h;
+}
+
 // One filter, keys [k0, k1), written to out + fo, in LDS windows of
 // kBloomWindowBytes (the path for filters a packed batch cannot hold).
 __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uint64_t fo,
@@ -231,32 +358,33 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
   if (lane == 0) *reinterpret_cast<gu8>(dst + bytes) = (uint8_t)a.k;  // :50
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // A wave takes kBloomGroup consecutive filters at a time.  When their keys
-// are contiguous and their bit arrays fit one LDS image (db_bench: 16 x 84 B),
-// the keys of all of them are spread over the 64 lanes round by round (33-key
-// filters would leave half the lanes idle at one filter per wave), each lane
-// finds its key's filter among the group, and every filter leaves LDS once.
-// Otherwise the group's filters go one by one through build_one.
+// are contiguous and their bit arrays fit the wave's LDS region (db_bench: 32 x
+// 84 B), the keys of all of them are spread over the 64 lanes round by round
+// (a 33-key filter would leave half the lanes idle at one filter per wave):
+// each lane finds its key's filter by a binary search over the group's first
+// keys (held one per lane, read with bpermute), takes that filter's bit-array
+// base, size and remainder constants from the filter's lane, and sets its k
+// bits with ds_or_b32 in the filter's part of the LDS image; every filter
+// leaves LDS once.  The round's key words are staged in the region's free
+// tail (wave_hash).  Otherwise the group's filters go one by one through
+// build_one.
 __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildArgs a) {
-  __shared__ uint32_t lds[kBloomWaves][kBloomWindowWords + 1];
-  __shared__ uint32_t slot_word[kBloomWaves][kBloomGroup], slot_d[kBloomWaves][kBloomGroup];
-  __shared__ uint64_t slot_m[kBloomWaves][kBloomGroup];
-  __shared__ uint32_t slot_c32[kBloomWaves][kBloomGroup];
+  // (rows of kBloomRegionWords: 16-B aligned, for the staging area's b128 writes)
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kBloomWaves][kBloomRegionWords];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* bm = lds[wv];
+  // Waves stride over groups of kBloomGroup consecutive filters.  (Tried:
+  // contiguous per-wave ranges, and a group size chosen so that every wave
+  // gets the same number of groups: 4% slower both)
   const uint64_t nwaves = (uint64_t)gridDim.x * kBloomWaves;
   const uint64_t n_groups = (a.n_filters + kBloomGroup - 1) / kBloomGroup;
+  const uint64_t kbase = reinterpret_cast<uint64_t>(a.keys);
   for (uint64_t grp = (uint64_t)blockIdx.x * kBloomWaves + wv; grp < n_groups; grp += nwaves) {
     const uint64_t f0 = grp * kBloomGroup;
     const uint32_t g = (uint32_t)(a.n_filters - f0 < kBloomGroup ? a.n_filters - f0 : kBloomGroup);
-    // lane j < g: filter f0 + j
+    // lane t < g: filter f0 + t
     uint64_t k0 = 0, k1 = 0, fo = 0, bytes = 0;
     if (lane < g) {
       k0 = a.filter_first[f0 + lane];
@@ -278,55 +406,64 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
     const uint64_t kb0 = readlane64(k0, 0), kb1 = readlane64(k1, g - 1);
     const uint64_t next0 = __shfl_down(k0, 1);
     const bool contiguous = lane >= g || (k1 >= k0 && (lane == g - 1 || next0 == k1));
-    const bool packed = __ballot(!contiguous) == 0 && total <= kBloomWindowWords &&
+    const bool packed = __ballot(!contiguous) == 0 && total <= kBloomRegionWords &&
                         kb1 >= kb0 && kb1 - kb0 < (1ull << 31);
     if (!packed) {
       for (uint32_t j = 0; j < g; j++)
         build_one(a, readlane64(k0, j), readlane64(k1, j), readlane64(fo, j), bm, lane);
       continue;
     }
-    const uint32_t base = (uint32_t)(incl - words);
-    if (lane < g) {
-      const uint32_t d = (uint32_t)(bytes * 8);
-      slot_word[wv][lane] = base;
-      slot_d[wv][lane] = d;
-      const uint64_t M = fastmod_magic(d);
-      slot_m[wv][lane] = M;
-      const uint32_t c = fastmod(0xffffffffu, M, d) + 1;  // 2^32 mod d
-      slot_c32[wv][lane] = c == d ? 0 : c;
-    }
-    for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
-    // first key (relative to the group's) of filters 1..g-1, wave-uniform
-    uint32_t st[kBloomGroup];
-#pragma unroll
-    for (uint32_t j = 1; j < kBloomGroup; j++)
-      st[j] = j < g ? (uint32_t)(readlane64(k0, j) - kb0) : 0xffffffffu;
-    wave_phase();
     const uint32_t nkeys = (uint32_t)(kb1 - kb0);
-    // The build is latency-bound (PMC: waves wait 74% of their cycles): the
-    // next round's key offsets are loaded while this round hashes, and a key's
-    // words are all requested at once (hash_key_batched).
+    // The build is latency-bound: the next round's key offsets are loaded
+    // while this round hashes.
     const uint64_t* ko = a.key_offsets + kb0;
     uint64_t o0 = 0, o1 = 0;
     if (lane < nkeys) {
       o0 = ko[lane];
       o1 = ko[lane + 1];
     }
-    for (uint32_t r = lane; r < nkeys; r += 64) {
-      uint32_t j = 0;
+    // filter t's constants, in lane t: LDS word base, bits d, fastmod magic,
+    // 2^32 mod d, and its first key relative to the group's (non-decreasing;
+    // ~0 past the group, so that a search never selects those lanes)
+    const uint32_t base_t = (uint32_t)(incl - words);
+    const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
+    const uint64_t m_t = fastmod_magic(d_t);
+    const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
+    const uint32_t c32_t = c == d_t ? 0u : c;
+    const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
+    for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
+    wave_phase();
+    // the staging area: the region's free tail, less 48 B that a key's hash
+    // may read past the span (none at all when the filters fill the region)
+    const uint32_t used = (uint32_t)((total + 3u) & ~3ull) * 4u;
+    uint32_t* stg = bm + used / 4u;
+    const uint32_t avail = used + 48u < kBloomRegionWords * 4u ? kBloomRegionWords * 4u - used - 48u : 0u;
+    for (uint32_t r0 = 0; r0 < nkeys; r0 += 64) {  // wave-uniform rounds
+      const uint32_t r = r0 + lane;
+      const bool act = r < nkeys;
+      // the last filter of the group whose first key is <= r (empty filters
+      // share their successor's first key and are passed over)
+      uint32_t pos = 1;  // (filter 0 starts at key 0)
 #pragma unroll
-      for (uint32_t t = 1; t < kBloomGroup; t++) j += r >= st[t] ? 1u : 0u;
-      const uint32_t wbase = slot_word[wv][j], d = slot_d[wv][j];
-      const uint64_t M = slot_m[wv][j];
-      const uint64_t s = reinterpret_cast<uint64_t>(a.keys) + o0;
-      const uint64_t n = o1 >= o0 + a.strip ? o1 - o0 - a.strip : 0;  // key_extent
+      for (uint32_t step = kBloomGroup / 2; step; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)st_t, (int)(pos + step - 1));
+        if (v <= r) pos += step;
+      }
+      const uint32_t j = pos - 1;
+      const uint32_t wbase = (uint32_t)__shfl((int)base_t, (int)j);
+      const uint32_t d = (uint32_t)__shfl((int)d_t, (int)j);
+      const uint64_t M = (uint64_t)__shfl((unsigned long long)m_t, (int)j);
+      const uint32_t c32 = (uint32_t)__shfl((int)c32_t, (int)j);
+      const uint64_t s = kbase + o0;
+      const uint64_t n = act && o1 >= o0 + a.strip ? o1 - o0 - a.strip : 0;  // key_extent
       if (r + 64 < nkeys) {
         o0 = ko[r + 64];
         o1 = ko[r + 65];
       }
-      uint32_t h = hash_key_batched(s, n, kBloomSeed);
+      const uint32_t h = wave_hash(stg, avail, s, n, act);
+      if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
-      ProbeSeq ps{fastmod(h, M, d), fastmod(delta, M, d), slot_c32[wv][j], d, h, delta};
+      ProbeSeq ps{fastmod(h, M, d), fastmod(delta, M, d), c32, d, h, delta};
       for (uint32_t q = 0; q < a.k; q++) {
         atomicOr(&bm[wbase + (ps.pos >> 5)], 1u << (ps.pos & 31u));
         ps.next();
@@ -336,7 +473,7 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
     for (uint32_t j = 0; j < g; j++) {
       const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + readlane64(fo, j);
       const uint32_t nb = (uint32_t)readlane64(bytes, j);
-      store_window(dst, bm + __builtin_amdgcn_readlane(base, j), nb, lane);
+      store_window(dst, bm + __builtin_amdgcn_readlane(base_t, j), nb, lane);
       if (lane == 0) *reinterpret_cast<gu8>(dst + nb) = (uint8_t)a.k;  // :50
     }
     wave_phase();
@@ -349,8 +486,7 @@ __device__ __forceinline__ uint64_t load_le32(uint64_t p) {  // DecodeFixed32, a
 }
 
 // util/bloom.cc:65-89 on the filter [f, f + len).
-__device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn,
-                              uint64_t k_use) {
+__device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_use) {
   if (len < 2) return false;
   // `array[len-1] > k_use_`: a signed char converted to size_t
   const uint64_t stored = (uint64_t)(int64_t)(int8_t)*reinterpret_cast<gcu8>(f + len - 1);
@@ -358,7 +494,6 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
   if (k > 30) return true;
   const uint64_t bits = (len - 1) * 8;
   const BitMod m = bit_mod(bits);
-  uint32_t h = hash_key_batched(ks, kn, kBloomSeed);
   const uint32_t delta = (h >> 17) | (h << 15);
   const bool inc = bits < (1ull << 31);  // ProbeSeq's range; else a remainder per probe
   ProbeSeq ps{0, 0, 0, (uint32_t)bits, h, delta};
@@ -375,12 +510,15 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
     uint32_t v[16], bit[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      const uint32_t bitpos = inc ? ps.pos : mod_bits(ps.h, m);
-      const bool live = j0 + j < (uint32_t)k;
-      bit[j] = live ? 1u << (bitpos & 7u) : 0u;
-      v[j] = live ? *reinterpret_cast<gcu8>(f + (bitpos >> 3)) : 0u;
-      if (inc) ps.next();
-      else ps.h += delta;
+      bit[j] = 0u;
+      v[j] = 0u;
+      if (j0 + j < (uint32_t)k) {  // (k is the same in every lane of a wave, in practice)
+        const uint32_t bitpos = inc ? ps.pos : mod_bits(ps.h, m);
+        bit[j] = 1u << (bitpos & 7u);
+        v[j] = *reinterpret_cast<gcu8>(f + (bitpos >> 3));
+        if (inc) ps.next();
+        else ps.h += delta;
+      }
     }
     bool all = true;
 #pragma unroll
@@ -390,17 +528,27 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint64_t ks, uint64_t kn
   return true;
 }
 
+constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 31-B keys + slack)
+
 __global__ __launch_bounds__(256) void bloom_probe_kernel(BloomProbeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t stage[4][kProbeStageWords];
+  uint32_t* stg = stage[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63u;
   uint32_t hits = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += stride) {
+  // wave-uniform rounds of 64 consecutive queries (the hash is a wave operation)
+  for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q0 < a.n; q0 += stride) {
+    const uint64_t q = q0 + lane;
+    const bool act = q < a.n;
+    uint64_t ks = reinterpret_cast<uint64_t>(a.keys), kn = 0;
+    if (act) key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
+    const uint32_t h = wave_hash(stg, kProbeStageWords * 4u - 48u, ks, kn, act);
+    if (!act) continue;
     const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * q];
     const uint64_t size = a.handles[2 * q + 1];
-    uint64_t ks, kn;
-    key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
     bool may;
     if (a.mode == kProbeFilter) {
-      may = key_may_match(c, size, ks, kn, a.k_use);
+      may = key_may_match(c, size, h, a.k_use);
     } else {
       // FilterBlockReader (table/filter_block.cc:78-109): "errors are treated
       // as potential matches"; base_lg is a size_t loaded from a char, and the
@@ -416,7 +564,7 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(BloomProbeArgs a) {
             const uint64_t start = load_le32(c + last_word + index * 4);
             const uint64_t limit = load_le32(c + last_word + index * 4 + 4);
             if (start <= limit && limit <= last_word)
-              may = key_may_match(c + start, limit - start, ks, kn, a.k_use);
+              may = key_may_match(c + start, limit - start, h, a.k_use);
             else if (start == limit)
               may = false;  // an empty filter matches nothing
           }
@@ -428,7 +576,7 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(BloomProbeArgs a) {
   }
   if (a.n_may) {  // one atomic per wave
     for (int o = 32; o; o >>= 1) hits += (uint32_t)__shfl_xor((int)hits, o);
-    if ((threadIdx.x & 63u) == 0 && hits) atomicAdd(a.n_may, hits);
+    if (lane == 0 && hits) atomicAdd(a.n_may, hits);
   }
 }
 
@@ -443,6 +591,36 @@ hipError_t launch_bloom_build(const BloomBuildArgs& a, int grid, hipStream_t str
 hipError_t launch_bloom_probe(const BloomProbeArgs& a, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(bloom_probe_kernel, dim3(grid), dim3(256), 0, stream, a);
   return hipGetLastError();
+}
+
+// Workgroups of each kernel resident per CU (registers, LDS): grid-stride
+// launches size their grids to fill the chip exactly once.
+int bloom_build_blocks_per_cu() {
+#ifdef LSBM_BUILD_WGS  // A/B builds only
+  return LSBM_BUILD_WGS;
+#endif
+  // Measured: 6 workgroups of this kernel are resident per CU although the
+  // occupancy query reports 7; a 7-per-CU grid ran 30% slower, as a second
+  // batch of workgroups (A/B 5/6/7/8).
+  return 6;
+  static const int v = [] {
+    int b = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, bloom_build_kernel, kBloomThreads, 0) ==
+                       hipSuccess && b > 0 ? b : 4;
+  }();
+  return v;
+}
+
+int bloom_probe_blocks_per_cu() {
+#ifdef LSBM_PROBE_WGS  // A/B builds only
+  return LSBM_PROBE_WGS;
+#endif
+  static const int v = [] {
+    int b = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, bloom_probe_kernel, 256, 0) == hipSuccess &&
+                       b > 0 ? b : 4;
+  }();
+  return v;
 }
 
 }  // namespace lsbm

@@ -288,6 +288,27 @@ def gpu_build(torch, keys, filters, bits_per_key, strip=0, gap=0):
 
 
 @pytest.mark.gpu
+def test_gpu_build_groups_that_fill_the_lds_region(torch_cuda, bloom_oracle):
+    """Groups of 32 filters whose bit arrays (nearly) fill a wave's LDS region
+    leave no room to stage key words: the staging capacity must come out as 0,
+    not wrap around (which let one wave's staging overwrite its neighbour's
+    filters, bloom_kernels.hip bloom_build_kernel)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    counts = rng.integers(112, 131, size=2000)  # 36-42 LDS words per filter at 10 bits/key
+    keys = random_keys(4242, int(counts.sum()), 8, 48)
+    filters, k = [], 0
+    for c in counts:
+        filters.append((k, k + int(c)))
+        k += int(c)
+    out, offs, sizes = gpu_build(torch, keys, filters, 10, 8, 3)
+    bad = [i for i, (k0, k1) in enumerate(filters)
+           if out[int(offs[i]):int(offs[i]) + sizes[i]].tobytes()
+           != bloom_oracle.create_filter(take(keys, range(k0, k1)), 10, 8)]
+    assert bad == []
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bits_per_key", [0, 1, 3, 10, 20, 45])
 @pytest.mark.parametrize("strip,gap", [(0, 0), (8, 3)])
 def test_gpu_build_matches_oracle(torch_cuda, bloom_oracle, bits_per_key, strip, gap):

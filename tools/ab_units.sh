@@ -1,17 +1,24 @@
-# A/B variants of the units kernel (build container: `tools/ab_units.sh build`;
+#!/bin/bash
+# A/B variants of one kernel file (build container: `tools/ab_units.sh build`;
 # GPU box: `tools/ab_units.sh run [configs...]`).  Each variant is the product
-# library with crc32c_kernels.hip rebuilt under extra -D flags; runs are
-# interleaved, two passes per variant.  VARIANTS="name:-DX+-DY ..." overrides.
+# library with that kernel file rebuilt under extra -D flags (or from another
+# source, SRC=...); runs are interleaved, two passes per variant.
+#   VARIANTS="name:-DX+-DY ..."   the variants
+#   KFILE=crc32c_kernels|bloom_kernels|snappy_kernels   (default crc32c_kernels)
+#   BENCH="python -u tools/bench_configs.py"            the command run per variant
 set -e
 cd "$(dirname "$0")/.."
-V=${VARIANTS:-"base: late:-DLSBM_STORE_LATE nostore:-DLSBM_DIAG_NO_STORE"}
-OBJS="build/csrc/crc32c_engine.o build/csrc/crc32c_host.o build/csrc/table_checksum.o build/csrc/log_checksum.o build/csrc/status.o build/csrc/bloom_kernels.o build/csrc/bloom_engine.o build/csrc/bloom_host.o build/csrc/filter_block.o build/csrc/snappy_kernels.o build/csrc/snappy_engine.o build/csrc/block_compression.o build/csrc/host_session.o"
+V=${VARIANTS:-"base:"}
+K=${KFILE:-crc32c_kernels}
+ALL="crc32c_kernels crc32c_engine crc32c_host table_checksum log_checksum status bloom_kernels bloom_engine bloom_host filter_block snappy_kernels snappy_engine block_compression host_session"
+OBJS=""
+for o in $ALL; do [ "$o" = "$K" ] || OBJS="$OBJS build/csrc/$o.o"; done
 if [ "$1" = build ]; then
   mkdir -p build/abl
   for v in $V; do
     name=${v%%:*}; flags=$(echo ${v#*:} | tr "+" " ")
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fvisibility=hidden $flags \
-      -c -o build/abl/k_$name.o ${SRC:-lsbm_amd/csrc/crc32c_kernels.hip} &
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fvisibility=hidden -munsafe-fp-atomics $flags \
+      -c -o build/abl/k_$name.o ${SRC:-lsbm_amd/csrc/$K.hip} &
   done
   wait
   for v in $V; do
@@ -24,7 +31,7 @@ else
     for v in $V; do
       name=${v%%:*}
       echo "== $name pass $pass"
-      LSBM_LIB_PATH=build/abl/lib_$name.so timeout -k 10 200 python -u tools/bench_configs.py ${@:-sst4118 config4}
+      LSBM_LIB_PATH=build/abl/lib_$name.so timeout -k 10 200 ${BENCH:-python -u tools/bench_configs.py} ${@:-sst4118 config4}
     done
   done
 fi

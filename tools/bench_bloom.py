@@ -13,8 +13,8 @@ resident in HBM before timing.  One JSON line per measurement:
 
 Algorithmic bytes (what the roofline fraction uses) are stated per line.
 cpu_baseline: the reference's own CreateFilter / KeyMayMatch
-(oracle/_ref/libref_bloom.so, built from /root/reference) on one host core,
-on a bounded sample, else the oracle's C restatement.
+(oracle/_ref/libref_bloom.so, built from /root/reference) on every usable
+host core and on one, on a bounded sample, else the oracle's C restatement.
 """
 import argparse
 import ctypes
@@ -46,7 +46,18 @@ def dbbench_keys_dev(torch, n, first=0, seq0=1):
     return out.reshape(-1)
 
 
-def timed(torch, fn, reps, warm=2):
+def timed(torch, fn, reps, warm=2, spin_s=None):
+    """Seconds per call, after spin_s seconds of untimed calls: after a host
+    pause the GPU clock has dropped.  LSBM_SPIN_S=0
+    under rocprofv3 --pmc."""
+    if spin_s is None:
+        spin_s = float(os.environ.get("LSBM_SPIN_S", "0.3"))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < spin_s:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -61,10 +72,15 @@ def timed(torch, fn, reps, warm=2):
 
 
 def cpu_baseline(sample_filters, seconds=4.0):
-    """The reference's own CreateFilter / KeyMayMatch loops (C, one thread) on
-    a bounded db_bench-shaped sample, repeated for about `seconds`; the
-    oracle's C restatement when the reference build is absent."""
+    """The reference's own CreateFilter / KeyMayMatch loops (C) on a bounded
+    db_bench-shaped sample, repeated for about `seconds`, on every usable host
+    core (one thread each: ctypes releases the GIL, every thread has its own
+    output), plus the one-core rate; the oracle's C restatement on one core
+    when the reference build is absent."""
+    import threading
     from golden.bloomkeys import dbbench_keys
+    sys.path.insert(0, REPO)
+    from bench import usable_cores
     n = sample_filters * PER
     first = np.minimum(np.arange(sample_filters + 1, dtype=np.uint64) * PER, n).astype(np.uint64)
     fidx = (np.arange(n) // PER).astype(np.uint64)
@@ -72,6 +88,7 @@ def cpu_baseline(sample_filters, seconds=4.0):
     out = np.zeros(sample_filters * 100, dtype=np.uint8)
     vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     ref = os.path.join(REPO, "oracle", "_ref", "libref_bloom.so")
+    threads = 1
     if os.path.exists(ref):
         lib, kind = ctypes.CDLL(ref), "reference"
         lib.ref_create_filters.restype = sz
@@ -80,14 +97,17 @@ def cpu_baseline(sample_filters, seconds=4.0):
         lib.ref_may_match_batch.argtypes = [i32, vp, vp, sz, vp, vp, vp]
         # InternalFilterPolicy hands the bloom policy user keys: 23 B
         keys, offs = dbbench_keys(0, n, internal=False)
+        threads = usable_cores()[0]
+        outs = [np.zeros_like(out) for _ in range(threads)]
+        fos = [np.zeros_like(fo) for _ in range(threads)]
 
-        def build():
+        def build(t=0):
             lib.ref_create_filters(BPK, keys.ctypes.data, offs.ctypes.data, first.ctypes.data,
-                                   sample_filters, out.ctypes.data, fo.ctypes.data)
+                                   sample_filters, outs[t].ctypes.data, fos[t].ctypes.data)
 
-        def probe():
+        def probe(t=0):
             return lib.ref_may_match_batch(BPK, keys.ctypes.data, offs.ctypes.data, n,
-                                           out.ctypes.data, fo.ctypes.data, fidx.ctypes.data)
+                                           outs[0].ctypes.data, fos[0].ctypes.data, fidx.ctypes.data)
     else:
         from conftest import BloomOracle
         o = BloomOracle(os.path.join(REPO, "oracle", "liboracle_bloom.so"))
@@ -96,35 +116,54 @@ def cpu_baseline(sample_filters, seconds=4.0):
         fsize = o.filter_bytes(PER, BPK)
         fo[:] = np.arange(sample_filters + 1, dtype=np.uint64) * fsize
 
-        def build():
+        def build(t=0):
             for f in range(sample_filters):
                 o.lib.bo_create_filter(keys.ctypes.data, offs[f * PER:].ctypes.data, PER, 8, BPK,
                                        out.ctypes.data + f * fsize)
 
-        def probe():
+        def probe(t=0):
             return sum(o.lib.bo_key_may_match(keys.ctypes.data + int(offs[i]), KLEN, 8,
                                               out.ctypes.data + int(fidx[i]) * fsize, fsize, BPK, 15)
                        for i in range(n))
 
-    def rate(fn):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            r = fn()
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 2:
-                return reps * n / el, r
-    build_rate, _ = rate(build)
-    probe_rate, hits = rate(probe)
+    def rate(fn, nt):
+        """keys per second over nt threads, each repeating fn for ~seconds / 4"""
+        reps = [0] * nt
+        res = [None] * nt
+        go = threading.Barrier(nt + 1)
+
+        def worker(t):
+            go.wait()
+            t0 = time.perf_counter()
+            while True:
+                res[t] = fn(t)
+                reps[t] += 1
+                if time.perf_counter() - t0 >= seconds / 4:
+                    return
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(nt)]
+        for th in ths:
+            th.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for th in ths:
+            th.join()
+        return sum(reps) * n / (time.perf_counter() - t0), res[0]
+    build(0)  # the filters probe() reads
+    build_1, _ = rate(build, 1)
+    probe_1, hits = rate(probe, 1)
+    build_all, _ = rate(build, threads) if threads > 1 else (build_1, None)
+    probe_all, _ = rate(probe, threads) if threads > 1 else (probe_1, None)
     cpu = ""
     try:
         cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except (OSError, IndexError):
         pass
-    return {"kind": kind, "cores": 1, "build_keys_per_s": round(build_rate, 1),
-            "probe_keys_per_s": round(probe_rate, 1), "members_found": int(hits) == n,
+    return {"kind": kind, "cores": threads, "build_keys_per_s": round(build_all, 1),
+            "probe_keys_per_s": round(probe_all, 1), "build_keys_per_s_1core": round(build_1, 1),
+            "probe_keys_per_s_1core": round(probe_1, 1), "members_found": int(hits) == n,
             "sample": f"{sample_filters} filters x {PER} db_bench keys, CreateFilter and "
-                      f"KeyMayMatch loops in C, one thread, ~{seconds:.0f} s; {cpu}"}
+                      f"KeyMayMatch loops in C, {threads} thread(s) (every usable core) and 1, "
+                      f"~{seconds:.0f} s; {cpu}"}
 
 
 def main():
@@ -189,7 +228,9 @@ def main():
             bloom.may_match(out, handles, keys, koffs, BPK, 15, strip=8, may=may, n_may=n_may)
 
         t = timed(torch, probe, args.reps)
-        found = int(n_may.item()) // (args.reps + 2)
+        n_may.zero_()
+        probe()
+        found = int(n_may.item())
         alg = n * (KLEN + 8 + 16 + 1 + bloom.k_probe(BPK, 15))
         gbps = alg / t / 1e9
         lines.append({"bench": "bloom_probe", "queries": n, "ms": round(t * 1e3, 3),
@@ -231,7 +272,9 @@ def main():
                                          may=may, n_may=n_may)
 
         t = timed(torch, block, args.reps)
-        found = int(n_may.item()) // (args.reps + 2)
+        n_may.zero_()
+        block()
+        found = int(n_may.item())
         alg = n * (KLEN + 8 + 16 + 8 + 1 + 8 + 1 + bloom.k_probe(BPK, 15))
         gbps = alg / t / 1e9
         lines.append({"bench": "bloom_block", "queries": n, "filter_blocks": nb,
