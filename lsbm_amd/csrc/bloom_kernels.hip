@@ -322,6 +322,62 @@ __device__ __forceinline__ uint32_t wave_hash(uint32_t* stg, uint32_t avail, uin
   return h;
 }
 
+// The build's key staging, pipelined one round ahead: a round's span is
+// planned (wave-uniform) and its 16-B chunks loaded into registers -- two per
+// lane, spans up to 2 KiB (64 db_bench keys: 1,984 B) -- during the round
+// before; the round then writes them to LDS and hashes from there, so no
+// round waits for its key words.  Spans that do not fit are hashed from
+// global memory (hash_key_batched).
+struct SpanPlan {
+  uint64_t sbase;  // 16-B aligned start (staged), or a safe 16-B aligned address
+  uint32_t nch;    // chunks, 0 when not staged
+};
+
+__device__ __forceinline__ SpanPlan plan_span(uint64_t s, uint64_t n, uint32_t cap, uint64_t safe) {
+  const uint64_t nz = __ballot(n > 0);
+  const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
+  const uint32_t ll = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
+  const uint64_t lo = readlane64(s, fl), hi = readlane64(s + n, ll);
+  const uint64_t sbase = lo & ~15ull;
+  const bool inside = n == 0 || (s >= lo && s + n <= hi);
+  const bool staged = nz != 0 && hi > lo && hi - sbase <= cap && hi - sbase <= 2048u &&
+                      __ballot(!inside) == 0ull;
+  SpanPlan p;
+  p.sbase = staged ? sbase : safe;
+  p.nch = staged ? (uint32_t)((hi - sbase + 15) >> 4) : 0u;
+  return p;
+}
+
+// Every lane loads (unconditionally, from a readable chunk) so that the loads
+// in flight are the same on every path.
+__device__ __forceinline__ void fetch_span(const SpanPlan& p, u32x4& c0, u32x4& c1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t a0 = lane < p.nch ? p.sbase + 16ull * lane : p.sbase;
+  const uint64_t a1 = lane + 64u < p.nch ? p.sbase + 16ull * (lane + 64u) : p.sbase;
+  c0 = *reinterpret_cast<gcu32x4>(a0);
+  c1 = *reinterpret_cast<gcu32x4>(a1);
+}
+
+__device__ __forceinline__ uint32_t staged_hash(uint32_t* stg, const SpanPlan& p, u32x4 c0, u32x4 c1,
+                                                uint64_t s, uint64_t n, bool act) {
+  const uint32_t lane = threadIdx.x & 63u;
+  if (p.nch == 0) return hash_key_batched(s, n, kBloomSeed);
+  if (lane < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * lane) = c0;
+  if (lane + 64u < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * (lane + 64u)) = c1;
+  wave_phase();
+  const uint64_t nz = __ballot(n > 0);
+  const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
+  const uint32_t rel = act ? (uint32_t)(s - p.sbase) : 0u;
+  const uint32_t n0 = (uint32_t)readlane64(n, fl);
+  uint32_t h;
+  if (__ballot(act && n != n0) == 0ull)
+    h = hash_key_lds_uniform(stg, rel, __builtin_amdgcn_readfirstlane(n0), kBloomSeed);
+  else
+    h = hash_key_lds(stg, rel, (uint32_t)n, kBloomSeed);
+  wave_phase();  // (the next round's staging writes after these reads)
+  return h;
+}
+
 // One filter, keys [k0, k1), written to out + fo, in LDS windows of
 // kBloomWindowBytes (the path for filters a packed batch cannot hold).
 __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uint64_t fo,
@@ -369,7 +425,13 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 // leaves LDS once.  The round's key words are staged in the region's free
 // tail (wave_hash).  Otherwise the group's filters go one by one through
 // build_one.
-__global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildArgs a) {
+#ifndef LSBM_BUILD_WAVES_PER_EU  // (A/B builds override)
+#define LSBM_BUILD_WAVES_PER_EU 7
+#endif
+// 7 waves per SIMD (<= 72 VGPRs): the grid is sized for 7 workgroups per CU
+// (A/B: 6 -> 0.372 ms, 7 -> 0.358 ms, 8 -> 0.419 ms with scratch spills)
+__global__ __launch_bounds__(kBloomThreads) __attribute__((amdgpu_waves_per_eu(LSBM_BUILD_WAVES_PER_EU)))
+void bloom_build_kernel(BloomBuildArgs a) {
   // (rows of kBloomRegionWords: 16-B aligned, for the staging area's b128 writes)
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBloomWaves][kBloomRegionWords];
   const uint32_t lane = threadIdx.x & 63u;
@@ -381,15 +443,27 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
   const uint64_t nwaves = (uint64_t)gridDim.x * kBloomWaves;
   const uint64_t n_groups = (a.n_filters + kBloomGroup - 1) / kBloomGroup;
   const uint64_t kbase = reinterpret_cast<uint64_t>(a.keys);
+  // lane t < g: filter f0 + t.  A group's filter table entries are loaded
+  // while the group before writes its filters out.
+  uint64_t mk0 = 0, mk1 = 0, mfo = 0;
+  auto load_meta = [&](uint64_t grp) {
+    const uint64_t f0 = grp * kBloomGroup;
+    mk0 = mk1 = mfo = 0;
+    if (grp < n_groups && lane < a.n_filters - f0 && lane < kBloomGroup) {
+      mk0 = a.filter_first[f0 + lane];
+      mk1 = a.filter_first[f0 + lane + 1];
+      mfo = a.filter_out[f0 + lane];
+    }
+  };
+  load_meta((uint64_t)blockIdx.x * kBloomWaves + wv);
   for (uint64_t grp = (uint64_t)blockIdx.x * kBloomWaves + wv; grp < n_groups; grp += nwaves) {
     const uint64_t f0 = grp * kBloomGroup;
     const uint32_t g = (uint32_t)(a.n_filters - f0 < kBloomGroup ? a.n_filters - f0 : kBloomGroup);
-    // lane t < g: filter f0 + t
     uint64_t k0 = 0, k1 = 0, fo = 0, bytes = 0;
+    k0 = mk0;  // (0 past the group)
+    k1 = mk1;
+    fo = mfo;
     if (lane < g) {
-      k0 = a.filter_first[f0 + lane];
-      k1 = a.filter_first[f0 + lane + 1];
-      fo = a.filter_out[f0 + lane];
       uint64_t bits = (k1 > k0 ? k1 - k0 : 0) * a.bits_per_key;
       if (bits < 64) bits = 64;
       bytes = (bits + 7) / 8;
@@ -409,18 +483,24 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
     const bool packed = __ballot(!contiguous) == 0 && total <= kBloomRegionWords &&
                         kb1 >= kb0 && kb1 - kb0 < (1ull << 31);
     if (!packed) {
+      load_meta(grp + nwaves);
       for (uint32_t j = 0; j < g; j++)
         build_one(a, readlane64(k0, j), readlane64(k1, j), readlane64(fo, j), bm, lane);
       continue;
     }
     const uint32_t nkeys = (uint32_t)(kb1 - kb0);
-    // The build is latency-bound: the next round's key offsets are loaded
-    // while this round hashes.
     const uint64_t* ko = a.key_offsets + kb0;
-    uint64_t o0 = 0, o1 = 0;
+    const uint64_t safe = reinterpret_cast<uint64_t>(ko) & ~15ull;  // a readable 16-B chunk
+    // Key offsets are loaded two rounds ahead and key words (staged) one
+    // round ahead: round r holds the offsets of rounds r and r + 1.
+    uint64_t oa0 = 0, oa1 = 0, ob0 = 0, ob1 = 0;
     if (lane < nkeys) {
-      o0 = ko[lane];
-      o1 = ko[lane + 1];
+      oa0 = ko[lane];
+      oa1 = ko[lane + 1];
+    }
+    if (lane + 64u < nkeys) {
+      ob0 = ko[lane + 64];
+      ob1 = ko[lane + 65];
     }
     // filter t's constants, in lane t: LDS word base, bits d, fastmod magic,
     // 2^32 mod d, and its first key relative to the group's (non-decreasing;
@@ -438,6 +518,14 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
     const uint32_t used = (uint32_t)((total + 3u) & ~3ull) * 4u;
     uint32_t* stg = bm + used / 4u;
     const uint32_t avail = used + 48u < kBloomRegionWords * 4u ? kBloomRegionWords * 4u - used - 48u : 0u;
+    SpanPlan plan;
+    u32x4 ch0, ch1;
+    {
+      const bool act = lane < nkeys;
+      const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
+      plan = plan_span(kbase + oa0, n, avail, safe);
+      fetch_span(plan, ch0, ch1);
+    }
     for (uint32_t r0 = 0; r0 < nkeys; r0 += 64) {  // wave-uniform rounds
       const uint32_t r = r0 + lane;
       const bool act = r < nkeys;
@@ -454,21 +542,36 @@ __global__ __launch_bounds__(kBloomThreads) void bloom_build_kernel(BloomBuildAr
       const uint32_t d = (uint32_t)__shfl((int)d_t, (int)j);
       const uint64_t M = (uint64_t)__shfl((unsigned long long)m_t, (int)j);
       const uint32_t c32 = (uint32_t)__shfl((int)c32_t, (int)j);
-      const uint64_t s = kbase + o0;
-      const uint64_t n = act && o1 >= o0 + a.strip ? o1 - o0 - a.strip : 0;  // key_extent
-      if (r + 64 < nkeys) {
-        o0 = ko[r + 64];
-        o1 = ko[r + 65];
+      const uint64_t s = kbase + oa0;
+      const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+      // this round's chunks into LDS, then the next round's plan and loads
+      const SpanPlan cur = plan;
+      const u32x4 cc0 = ch0, cc1 = ch1;
+      {
+        const bool act1 = r + 64u < nkeys;
+        const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
+        plan = plan_span(kbase + ob0, n1, avail, safe);
+        fetch_span(plan, ch0, ch1);
+        oa0 = ob0;
+        oa1 = ob1;
+        if (r + 128u < nkeys) {
+          ob0 = ko[r + 128];
+          ob1 = ko[r + 129];
+        }
       }
-      const uint32_t h = wave_hash(stg, avail, s, n, act);
+      const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
       if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
       ProbeSeq ps{fastmod(h, M, d), fastmod(delta, M, d), c32, d, h, delta};
+#ifdef LSBM_PROBE_UNROLL  // A/B builds only
+#pragma unroll LSBM_PROBE_UNROLL
+#endif
       for (uint32_t q = 0; q < a.k; q++) {
         atomicOr(&bm[wbase + (ps.pos >> 5)], 1u << (ps.pos & 31u));
         ps.next();
       }
     }
+    load_meta(grp + nwaves);
     wave_phase();
     for (uint32_t j = 0; j < g; j++) {
       const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + readlane64(fo, j);
@@ -530,7 +633,12 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
 
 constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 31-B keys + slack)
 
-__global__ __launch_bounds__(256) void bloom_probe_kernel(BloomProbeArgs a) {
+#ifdef LSBM_PROBE_WAVES_PER_EU  // A/B builds only
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSBM_PROBE_WAVES_PER_EU)))
+#else
+__global__ __launch_bounds__(256)
+#endif
+void bloom_probe_kernel(BloomProbeArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stage[4][kProbeStageWords];
   uint32_t* stg = stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63u;
@@ -599,10 +707,11 @@ int bloom_build_blocks_per_cu() {
 #ifdef LSBM_BUILD_WGS  // A/B builds only
   return LSBM_BUILD_WGS;
 #endif
-  // Measured: 6 workgroups of this kernel are resident per CU although the
-  // occupancy query reports 7; a 7-per-CU grid ran 30% slower, as a second
-  // batch of workgroups (A/B 5/6/7/8).
-  return 6;
+  // = LSBM_BUILD_WAVES_PER_EU (one wave per SIMD per workgroup).  Measured:
+  // without the waves-per-EU bound the kernel took 79-95 VGPRs and only 6
+  // workgroups fitted although the occupancy query reported 7; a 7-per-CU
+  // grid then ran 30% slower, as a second batch.
+  return LSBM_BUILD_WAVES_PER_EU;
   static const int v = [] {
     int b = 0;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, bloom_build_kernel, kBloomThreads, 0) ==
