@@ -165,6 +165,41 @@ def test_ragged_byte_balanced_ranges_skewed(torch_cuda, oracle, kind):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mode", ["extents", "sst_crcs"])
+def test_ragged_units_gigabytes_apart(torch_cuda, oracle, mode):
+    """Consecutive blocks ~3 GiB apart: a round's units do not fit one 2 GiB
+    buffer window, so the units kernel takes one window per pass (rows are
+    loaded through bounded buffer descriptors, crc32c_kernels.hip)."""
+    torch = torch_cuda
+    from lsbm_amd import engine, table
+    total = (3 << 30) + (40 << 20)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 606)
+    rng = np.random.default_rng(31)
+    n = 3000
+    lens = rng.integers(0, 9000, size=n)
+    starts = np.where(np.arange(n) % 3 == 1, 3 << 30, 7) + np.arange(n) * 251 * 40
+    starts = starts + rng.integers(0, 64, size=n)
+    ext = np.stack([starts, lens], 1).reshape(-1).astype(np.int64)
+    try:
+        if mode == "extents":
+            want = np.array([oracle.value(stream_bytes(606, int(s), int(l)).tobytes())
+                             for s, l in zip(starts, lens)], dtype=np.uint32)
+            got = _u32(engine.crc32c_extents(d, _dev(torch, ext)))
+        else:  # WriteRawBlock's crc of block || type, the type byte being the byte after the block
+            types = rng.integers(0, 2, size=n).astype(np.uint8)
+            want = np.array([oracle.mask(oracle.extend(oracle.value(stream_bytes(606, int(s), int(l)).tobytes()),
+                                                       bytes([int(t)])))
+                             for s, l, t in zip(starts, lens, types)], dtype=np.uint32)
+            out, nbad = table.trailer_crcs(d, _dev(torch, ext), _dev(torch, types))
+            assert int(nbad.item()) == 0
+            got = _u32(out)
+        assert np.array_equal(got, want)
+    finally:
+        del d
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("order", ["random", "descending"])
 def test_ragged_unsorted_starts_tile_exactly(torch_cuda, oracle, order):
     """The byte cut on a batch whose starts are not sorted: the search is
