@@ -898,6 +898,56 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
 }
 
 // ---------------------------------------------------------------------------
+// Trailer scatter: the second pass of lsbm_sst_seal_dev.  The units kernel
+// computes the CRCs densely (SstCrc mode); this pass merges trailer i =
+// [types[i]][crc LE32] into file[off + size, +5) for every handle that fits.
+// Each merge is a compare-and-swap on the aligned 8-byte word(s) covering the
+// bytes (correct when records shorter than 11 bytes share a word).  Measured
+// on 1M x 4,118-B blocks: the scattered 5-byte writes cost the read-streaming
+// kernel 13 points of HBM bandwidth when done in it, and a separate pass of
+// byte stores as much again (0.17 ms); the compare-and-swap pass, ~0.03 ms.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cas_merge(unsigned long long* p, uint64_t m, uint64_t v) {
+  unsigned long long old = *p;
+  for (;;) {
+    const unsigned long long want = (old & ~m) | (v & m);
+    if (want == old) return;
+    const unsigned long long got = atomicCAS(p, old, want);
+    if (got == old) return;
+    old = got;
+  }
+}
+
+// nb (<= 5) little-endian bytes of v at address t of the image [img, img + limit)
+__device__ __forceinline__ void merge_bytes(uint64_t img, uint64_t limit, uint64_t t, uint32_t nb, uint64_t v) {
+  const uint32_t sh = (uint32_t)(t & 7u);
+  const uint64_t w0a = t & ~7ull;
+  const bool two = sh + nb > 8;
+  if (w0a < img || w0a + (two ? 16u : 8u) > img + limit) {  // words reaching outside: bytes
+    uint8_t* tb = reinterpret_cast<uint8_t*>(t);
+    for (uint32_t k = 0; k < nb; k++) tb[k] = (uint8_t)(v >> (8 * k));
+    return;
+  }
+  const uint64_t fm = (1ull << (8 * nb)) - 1;
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(w0a);
+  cas_merge(w, fm << (8 * sh), v << (8 * sh));
+  if (two) cas_merge(w + 1, fm >> (64 - 8 * sh), v >> (64 - 8 * sh));
+}
+
+__global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ file, uint64_t limit,
+                                                              const uint64_t* __restrict__ handles,
+                                                              const uint8_t* __restrict__ types,
+                                                              const uint32_t* __restrict__ crcs, uint64_t n) {
+  const uint64_t img = reinterpret_cast<uint64_t>(file);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t off = handles[2 * i], size = handles[2 * i + 1];
+    if (!(off <= limit && limit - off >= kTrailer && limit - off - kTrailer >= size)) continue;
+    merge_bytes(img, limit, img + off + size, 5, (uint64_t)types[i] | ((uint64_t)crcs[i] << 8));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Gather: dst[dst_off[i], +len[i]) = src[src_off[i], +len[i]), one wave per
 // segment (grid-stride), 16-B stores where both sides allow, bytes elsewhere.
 // Compacts variable-length outputs before they go back to the host
@@ -1042,6 +1092,14 @@ hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
       return hipErrorInvalidValue;
   }
 #undef LSBM_LAUNCH_UNITS
+  return hipGetLastError();
+}
+
+hipError_t launch_trailer_scatter(uint8_t* file, uint64_t limit, const uint64_t* handles, const uint8_t* types,
+                                  const uint32_t* crcs, uint64_t n, int grid, hipStream_t stream) {
+  const uint64_t want = (n + 255) / 256;
+  hipLaunchKernelGGL(trailer_scatter_kernel, dim3((unsigned)(want < (uint64_t)grid ? want : grid)), dim3(256), 0,
+                     stream, file, limit, handles, types, crcs, n);
   return hipGetLastError();
 }
 

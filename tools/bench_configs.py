@@ -324,6 +324,57 @@ def config1(args):
                               "fwrite on one thread (SURVEY.md 3.5)"}), flush=True)
 
 
+def wal(args):
+    """A WAL group commit on the device: 400K db_bench-sized records (0-2540 B,
+    ~0.5 GB framed), every header sealed (lsbm_log_seal_dev, with and without
+    the dense CRC output), the dense CRCs alone (lsbm_log_crcs_dev) and the
+    recovery check (lsbm_log_verify_dev).  Bytes = type + payload per header."""
+    import ctypes
+    import torch
+    from golden.splitmix import printable_bytes
+    from lsbm_amd import log
+    from lsbm_amd._lib import lib
+    rng = np.random.default_rng(0xA1)
+    lens = rng.integers(0, 2541, size=args.wal_records)
+    pay = printable_bytes(0xA2, int(lens.sum()))
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    wimg, heads = log.layout_records(pay[offs[i]:offs[i + 1]] for i in range(lens.size))
+    d = torch.from_numpy(wimg).to("cuda")
+    dh = torch.from_numpy(heads).to("cuda")
+    n = heads.size
+    masked = torch.empty(n, dtype=torch.int32, device="cuda")
+    nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(s.cuda_stream)
+    L = lib()
+    dp, hp, mp, bp, op = (ctypes.c_void_p(t.data_ptr()) for t in (d, dh, masked, nbad, ok))
+    nb = ctypes.c_uint64(d.numel())
+    t_seal = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hp, n, mp, bp, sp), s)
+    t_seal_nm = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hp, n, None, bp, sp), s)
+    t_crcs = time_launches(lambda: L.lsbm_log_crcs_dev(dp, nb, hp, n, mp, bp, sp), s)
+    nbad.zero_()
+    t_ver = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hp, n, op, bp, sp), s)
+    torch.cuda.synchronize()
+    img = d.cpu().numpy()
+    plen = img[heads + 4].astype(np.int64) | (img[heads + 5].astype(np.int64) << 8)
+    crc_bytes = int(plen.sum()) + n
+    o = oracle()
+    bad = 0
+    for i in range(0, n, max(1, n // 2000)):
+        h = int(heads[i])
+        want = o.mask(o.value(img[h + 6:h + 7 + int(plen[i])].tobytes()))
+        bad += int(want != int.from_bytes(img[h:h + 4].tobytes(), "little"))
+    pct = lambda t: round(crc_bytes / t / 1e9 / HBM * 100, 2)
+    print(json.dumps({"config": "wal", "records": int(lens.size), "physical": int(n), "crc_bytes": crc_bytes,
+                      "log_seal": {"ms": round(t_seal * 1e3, 3), "pct_hbm_peak": pct(t_seal)},
+                      "log_seal_no_out": {"ms": round(t_seal_nm * 1e3, 3), "pct_hbm_peak": pct(t_seal_nm)},
+                      "log_crcs": {"ms": round(t_crcs * 1e3, 3), "pct_hbm_peak": pct(t_crcs)},
+                      "log_verify": {"ms": round(t_ver * 1e3, 3), "pct_hbm_peak": pct(t_ver),
+                                     "all_ok": bool(ok.all().item())},
+                      "sample_mismatches": bad}), flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("which", nargs="*", default=["config1", "config3", "config4", "host"])
@@ -331,13 +382,15 @@ def main():
     p.add_argument("--c4-blocks", type=int, default=10_000_000)
     p.add_argument("--host-blocks", type=int, default=1 << 18)
     p.add_argument("--sst-blocks", type=int, default=1 << 20)
+    p.add_argument("--wal-records", type=int, default=400_000)
     args = p.parse_args()
     import torch
     torch.cuda.set_device(0)
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "config1": config1, "config3": config3, "config4": config4, "host": host_staged}[w](args)
+        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "config1": config1, "config3": config3, "config4": config4, "host": host_staged,
+         "wal": wal}[w](args)
 
 
 if __name__ == "__main__":
