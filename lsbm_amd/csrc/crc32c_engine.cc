@@ -481,7 +481,9 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   // trailer writes interleaved with the reads cost 13 points).  Without
   // scratch: in place, one pass.
   uint32_t* crcs = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&crcs), n_blocks * sizeof(uint32_t), s) != hipSuccess) {
+  static const bool one_pass = getenv("LSBM_SEAL_ONE_PASS") != nullptr;  // (A/B measurements)
+  if (one_pass ||
+      hipMallocAsync(reinterpret_cast<void**>(&crcs), n_blocks * sizeof(uint32_t), s) != hipSuccess) {
     (void)hipGetLastError();
     a.file = d_file;
     a.mode = kModeSstSeal;

@@ -552,7 +552,10 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       // scattered writes cost ~13% of HBM peak (A/B: the same 4-byte writes
       // added to verify took it from 75% to 62%; whole 64-B line writes were
       // no better): lsbm_sst_trailer_crcs_dev returns dense CRCs instead.
-      if (li < kTrailer)  // (non-temporal stores: no different, A/B)
+      // (non-temporal stores, and no-return atomic and/or merges of whole
+      // words: no different, A/B; lsbm_sst_seal_dev uses this mode only
+      // when it cannot have scratch for its two-pass seal)
+      if (li < kTrailer)
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(li == 0 ? typ : m >> (8 * (li - 1)));
     } else if constexpr (mode == kModeSstCrc) {  // the same crc, dense: out[b]
       const uint32_t typ = paux0 & 0xffu;
