@@ -111,6 +111,31 @@ int main() {
   s = lsbm::UncompressBlocks(0, contents.data(), coff.data(), bad.data(), n, &back, &boff, &ok);
   EXPECT(s.ToString() == "Corruption: bad block type");
 
+  // a block whose preamble claims 4 GiB among good ones: no 4 GiB window,
+  // that block alone fails (it cannot expand 22x beyond its compressed size)
+  {
+    std::string mixed;
+    std::vector<uint64_t> moff(1, 0);
+    std::vector<uint8_t> mtypes;
+    const size_t m = std::min<size_t>(n, 64), huge = m / 2;
+    for (size_t i = 0; i < m; i++) {
+      if (i == huge) {
+        mixed += std::string("\xff\xff\xff\xff\x0f", 5) + std::string(40, 'a');
+        mtypes.push_back(lsbm::kSnappyCompression);
+      } else {
+        mixed.append(contents, coff[i], coff[i + 1] - coff[i]);
+        mtypes.push_back(types[i]);
+      }
+      moff.push_back(mixed.size());
+    }
+    s = lsbm::UncompressBlocks(0, mixed.data(), moff.data(), mtypes.data(), m, &back, &boff, &ok);
+    EXPECT(s.ToString() == "Corruption: corrupted compressed block contents");
+    for (size_t i = 0; i < m; i++) EXPECT(ok[i] == (i == huge ? 0 : 1));
+    EXPECT(back.size() < (64u << 20));
+    for (size_t i = 0; i < m; i++)
+      if (i != huge) EXPECT(back.substr(boff[i], boff[i + 1] - boff[i]) == raw.substr(off[i], off[i + 1] - off[i]));
+  }
+
   if (fails) {
     printf("FAILED %d\n", fails);
     return 1;

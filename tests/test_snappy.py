@@ -202,6 +202,26 @@ def test_gpu_uncompressed_length(torch_cuda, snappy_oracle):
 
 
 @pytest.mark.gpu
+def test_gpu_uncompress_huge_preamble_among_good_blocks(torch_cuda, snappy_oracle):
+    """A preamble claiming 4 GiB (more than snappy's 22x expansion of its
+    compressed bytes allows) gets no window and fails alone; the good blocks
+    around it decode (lsbm_amd/snappy.py MAX_EXPANSION)."""
+    from lsbm_amd import snappy
+    good = [block("records", 4117 + i, 60000 + i) for i in range(6)]
+    streams = [snappy_oracle.compress(b) for b in good]
+    streams.insert(3, varint32(0xFFFFFFFF) + b"a" * 40)
+    data, offs = _pack(streams)
+    out, out_offsets, ok, n_bad = snappy.uncompress(_dev(torch_cuda, data), _dev(torch_cuda, offs))
+    assert out.numel() < (1 << 20)
+    okh = ok.cpu().numpy().tolist()
+    assert okh == [1, 1, 1, 0, 1, 1, 1] and int(n_bad.item()) == 1
+    oo = out_offsets.cpu().numpy()
+    outh = out.cpu().numpy()
+    for j, i in enumerate([0, 1, 2, 4, 5, 6]):
+        assert outh[oo[i]:oo[i + 1]].tobytes() == good[j]
+
+
+@pytest.mark.gpu
 def test_gpu_capacity_below_preamble_fails(torch_cuda, snappy_oracle):
     c = snappy_oracle.compress(b"abcd" * 1000)
     got = gpu_uncompress(torch_cuda, [c, c], caps=np.array([3999, 4000], dtype=np.int64))
