@@ -260,6 +260,81 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
   return op == ulen;
 }
 
+// decode<true> with the tag headers parsed 64 input bytes at a time: every
+// lane parses the tag that WOULD start at its byte of the window (kind, header
+// size, length, offset; all lanes at once, from the staged LDS copy), and the
+// wave then walks the real tags through the window reading each one's fields
+// from its lane (readlane: scalar registers) -- the serial part per tag is the
+// validity checks and the byte move, not the header decode.  Same checks in
+// the same order as decode(), so the same streams are rejected.
+__device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
+  uint32_t ip = 0, op = 0;
+  while (ip < cl) {
+    // parse the window [ip, ip + 64): lane l the tag at ip + l (bytes past the
+    // stream are the zero pad or the output slice; only tags whose checks fail
+    // ever use them)
+    const uint64_t w = load8<true>(in, ip + lane, cl);
+    const uint32_t c = (uint32_t)w & 0xffu;
+    const uint32_t kind = c & 3u;
+    uint32_t hdr, len, off = 0;
+    if (kind == 0) {
+      const uint32_t len0 = (c >> 2) + 1;
+      const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;
+      const uint64_t m = nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1);
+      const uint64_t lx = ((w >> 8) & m) + 1;  // (nb = 0: m = 0, lx = 1)
+      len = nb ? (lx > 0xffffffffull ? 0xffffffffu : (uint32_t)lx) : len0;  // (saturated: fails anyway)
+      hdr = 1 + nb;
+    } else if (kind == 1) {
+      hdr = 2;
+      len = 4 + ((c >> 2) & 7u);
+      off = ((c >> 5) << 8) | (uint32_t)((w >> 8) & 0xffu);
+    } else if (kind == 2) {
+      hdr = 3;
+      len = (c >> 2) + 1;
+      off = (uint32_t)((w >> 8) & 0xffffu);
+    } else {
+      hdr = 5;
+      len = (c >> 2) + 1;
+      off = (uint32_t)((w >> 8) & 0xffffffffu);
+    }
+    const uint32_t meta = kind | (hdr << 2);
+    // walk the tags that start inside this window
+    uint32_t s = 0;
+    while (s < 64u && ip < cl) {
+      const uint32_t mt = __builtin_amdgcn_readlane(meta, s);
+      const uint32_t tlen = __builtin_amdgcn_readlane(len, s);
+      const uint32_t th = mt >> 2;
+      if ((mt & 3u) == 0) {  // literal
+        if (th > 1 && th - 1 > cl - ip - 1) return false;
+        if (tlen > cl - ip - th || tlen > ulen - op) return false;
+        const uint8_t* src = in + ip + th;
+        uint8_t* dst = out + op;
+        for (uint32_t j = lane; j < tlen; j += 64) dst[j] = src[j];
+        ip += th + tlen;
+        op += tlen;
+        s += th + tlen;  // (a long literal ends the window)
+      } else {  // copy
+        const uint32_t toff = __builtin_amdgcn_readlane(off, s);
+        if (th > cl - ip || toff == 0 || toff > op || tlen > ulen - op) return false;
+        // byte j of the copy is out[op - off + j mod off]: an overlapping copy
+        // (off < len) repeats its first off bytes, all written before it.
+        if (lane < tlen) {
+          const uint32_t k = toff >= tlen ? lane : lane % toff;
+          out[op + lane] = out[op - toff + k];
+        }
+        ip += th;
+        op += tlen;
+        s += th;
+      }
+      // one wave's LDS accesses execute in issue order: a copy reads the bytes
+      // earlier tags wrote without waiting; this only keeps the compiler from
+      // reordering them
+      wave_order();
+    }
+  }
+  return op == ulen;
+}
+
 // Decodes block b with the wave's LDS slice of kSlice bytes when its
 // compressed bytes and output fit, else (kGlobalFallback) against global
 // memory.  Returns 2 when the block neither fits nor may fall back.
@@ -287,7 +362,11 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     uint8_t* win = smem + cl_pad;
     wave_phase();
     SNAP_STAMP(1);
+#ifdef LSBM_SNAP_SERIAL_DECODE  // A/B builds only
     ok = decode<true>(lds_in, cl, win, ulen, lane);
+#else
+    ok = decode_windowed(lds_in, cl, win, ulen, lane);
+#endif
     SNAP_STAMP(2);
 #ifndef LSBM_SNAP_DIAG_NO_OUT  // diagnostic build only (tools/snappy_diag.py): skips the output, wrong results
     if (ok) unstage_from_lds(a.out + os, win, ulen, lane);

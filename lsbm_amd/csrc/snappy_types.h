@@ -12,8 +12,13 @@ namespace lsbm {
 // LDS).
 constexpr uint32_t kSnapThreads = 64;
 // decoder slices hold the compressed bytes + 8 pad + the output window: pass 1
-// uses small slices (more waves in flight), pass 2 large ones
-constexpr uint32_t kSnapDecLds = 8192;
+// uses small slices (more waves in flight), pass 2 large ones.  7 KiB: a
+// db_bench block (4,117-4,122 B) with its compressed form (~2.3 KB) fits, 22
+// waves per CU (A/B: 8 KiB 171 GB/s, 7 KiB 189 GB/s, 6.5 KiB 187 GB/s).
+#ifndef LSBM_SNAP_DEC_LDS  // (A/B builds override)
+#define LSBM_SNAP_DEC_LDS 7168
+#endif
+constexpr uint32_t kSnapDecLds = LSBM_SNAP_DEC_LDS;
 constexpr uint32_t kSnapDecLdsLarge = 16384;
 // encoder: hash table (2 B/entry) + fragment bytes in a 22 KiB slice (a
 // 4 KiB block with its 8,192-entry table needs 20.1 KiB), then the match

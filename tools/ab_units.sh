@@ -31,7 +31,11 @@ else
     for v in $V; do
       name=${v%%:*}
       echo "== $name pass $pass"
-      LSBM_LIB_PATH=build/abl/lib_$name.so timeout -k 10 200 ${BENCH:-python -u tools/bench_configs.py} ${@:-sst4118 config4}
+      if [ -n "$BENCH" ]; then
+        LSBM_LIB_PATH=build/abl/lib_$name.so timeout -k 10 200 $BENCH "$@"
+      else
+        LSBM_LIB_PATH=build/abl/lib_$name.so timeout -k 10 200 python -u tools/bench_configs.py ${@:-sst4118 config4}
+      fi
     done
   done
 fi

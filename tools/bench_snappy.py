@@ -36,7 +36,17 @@ sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 HBM = 8000.0  # GB/s, MI355X spec
 
 
-def timed(torch, fn, reps, warm=2):
+def timed(torch, fn, reps, warm=2, spin_s=None):
+    """Seconds per call, after spin_s seconds of untimed calls (the GPU clock
+    drops during host-side pauses).  LSBM_SPIN_S=0 under
+    rocprofv3 --pmc."""
+    if spin_s is None:
+        spin_s = float(os.environ.get("LSBM_SPIN_S", "0.3"))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < spin_s:
+        fn()
+        torch.cuda.synchronize()
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
