@@ -391,7 +391,7 @@ __device__ __forceinline__ void record(const SnapDecArgs& a, uint64_t b, uint32_
 }
 
 // Pass 1: every block that fits a small slice (a db_bench data block and its
-// compressed form need < 8 KiB), at kSnapDecWgsPerCu waves per CU; the rest
+// compressed form need < 7 KiB), at kSnapDecWgsPerCu waves per CU; the rest
 // are marked ok = 2 for pass 2.
 __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_kernel(SnapDecArgs a) {
   const uint32_t lane = threadIdx.x;
