@@ -300,6 +300,8 @@ __device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, ui
     const uint32_t meta = kind | (hdr << 2);
     // walk the tags that start inside this window
     uint32_t s = 0;
+    // (one path for both kinds, the checks and byte move selected: 16%
+    // slower, A/B profiles/r02/snappy/ab_walk_single_path.log)
     while (s < 64u && ip < cl) {
       const uint32_t mt = __builtin_amdgcn_readlane(meta, s);
       const uint32_t tlen = __builtin_amdgcn_readlane(len, s);
