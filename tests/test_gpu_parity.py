@@ -624,15 +624,17 @@ def test_sst_handles_past_the_image(torch_cuda, oracle):
             assert tch[i] == int.from_bytes(out[off + sz + 1:off + sz + 5].tobytes(), "little")
 
 
-@pytest.mark.parametrize("seed,smax", [(31, 130), (32, 70), (33, 5000)])
-def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax):
-    """Every trailer of a table whose blocks are 0..smax bytes: the seal writes
-    whole 64-B lines only where no other trailer shares them, bytes otherwise;
-    all trailers and every byte between them must come out exactly right."""
+@pytest.mark.parametrize("seed,smax,n", [(31, 130, 20000), (32, 70, 20000), (33, 5000, 20000),
+                                         (34, 130, 150000), (35, 12, 150000)])
+def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax, n):
+    """Every trailer of a table whose blocks are 0..smax bytes: all trailers
+    and every byte between and after them must come out exactly right.  From
+    131,072 blocks on the seal is two passes, the second merging trailers by
+    compare-and-swap on 8-byte words that several tiny blocks' trailers share
+    (crc32c_kernels.hip trailer_scatter_kernel); below, one pass."""
     torch = torch_cuda
     from lsbm_amd import table
     rng = np.random.default_rng(seed)
-    n = 20000
     sizes = rng.integers(0, smax, size=n)
     sizes[rng.random(n) < 0.1] = 4118
     handles, total = table.layout_blocks(sizes)
