@@ -322,6 +322,16 @@ __device__ __forceinline__ uint32_t wave_hash(uint32_t* stg, uint32_t avail, uin
   return h;
 }
 
+// key_offsets[i] and [i + 1] with one 16-byte load (8-byte aligned: gfx950
+// global loads take any 4-byte aligned address)
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load_off2(const uint64_t* ko, uint64_t i, uint64_t& o0, uint64_t& o1) {
+  typedef const __attribute__((address_space(1), aligned(8))) u64x2* gp;
+  const u64x2 v = *reinterpret_cast<gp>(reinterpret_cast<uint64_t>(ko + i));
+  o0 = v.x;
+  o1 = v.y;
+}
+
 // The build's key staging, pipelined one round ahead: a round's span is
 // planned (wave-uniform) and its 16-B chunks loaded into registers -- two per
 // lane, spans up to 2 KiB (64 db_bench keys: 1,984 B) -- during the round
@@ -420,7 +430,7 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 // (a 33-key filter would leave half the lanes idle at one filter per wave):
 // each lane finds its key's filter by a binary search over the group's first
 // keys (held one per lane, read with bpermute), takes that filter's bit-array
-// base, size and remainder constants from the filter's lane, and sets its k
+// base, size and remainder constants from the filter's LDS slot, and sets its k
 // bits with ds_or_b32 in the filter's part of the LDS image; every filter
 // leaves LDS once.  The round's key words are staged in the region's free
 // tail (wave_hash).  Otherwise the group's filters go one by one through
@@ -434,6 +444,14 @@ __global__ __launch_bounds__(kBloomThreads) __attribute__((amdgpu_waves_per_eu(L
 void bloom_build_kernel(BloomBuildArgs a) {
   // (rows of kBloomRegionWords: 16-B aligned, for the staging area's b128 writes)
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBloomWaves][kBloomRegionWords];
+  // the group's filter constants, one slot per filter: LDS word base, bits d,
+  // fastmod magic (lo, hi); and 2^32 mod d.  (Read by index rather than with
+  // bpermute from the filter's lane: 5 fewer VGPRs live across the rounds,
+  // 0.354 -> 0.348 ms, profiles/r02/bloom/ab_slots.log.)
+  __shared__ __attribute__((aligned(16))) uint4 slots[kBloomWaves][kBloomGroup];
+  __shared__ uint32_t slot_c32[kBloomWaves][kBloomGroup];
+  static_assert(LSBM_BUILD_WAVES_PER_EU * (sizeof(lds) + sizeof(slots) + sizeof(slot_c32)) <= 160u * 1024u,
+                "the build grid's workgroups per CU must fit one CU's LDS");
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* bm = lds[wv];
@@ -494,22 +512,19 @@ void bloom_build_kernel(BloomBuildArgs a) {
     // Key offsets are loaded two rounds ahead and key words (staged) one
     // round ahead: round r holds the offsets of rounds r and r + 1.
     uint64_t oa0 = 0, oa1 = 0, ob0 = 0, ob1 = 0;
-    if (lane < nkeys) {
-      oa0 = ko[lane];
-      oa1 = ko[lane + 1];
-    }
-    if (lane + 64u < nkeys) {
-      ob0 = ko[lane + 64];
-      ob1 = ko[lane + 65];
-    }
-    // filter t's constants, in lane t: LDS word base, bits d, fastmod magic,
-    // 2^32 mod d, and its first key relative to the group's (non-decreasing;
+    if (lane < nkeys) load_off2(ko, lane, oa0, oa1);
+    if (lane + 64u < nkeys) load_off2(ko, lane + 64, ob0, ob1);
+    // filter t's constants, from lane t, into slot t: LDS word base, bits d,
+    // fastmod magic, 2^32 mod d; and (in lane t) its first key relative to the group's (non-decreasing;
     // ~0 past the group, so that a search never selects those lanes)
     const uint32_t base_t = (uint32_t)(incl - words);
-    const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
-    const uint64_t m_t = fastmod_magic(d_t);
-    const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
-    const uint32_t c32_t = c == d_t ? 0u : c;
+    if (lane < kBloomGroup) {
+      const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
+      const uint64_t m_t = fastmod_magic(d_t);
+      const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
+      slots[wv][lane] = make_uint4(base_t, d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
+      slot_c32[wv][lane] = c == d_t ? 0u : c;
+    }
     const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
     for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
     wave_phase();
@@ -538,10 +553,10 @@ void bloom_build_kernel(BloomBuildArgs a) {
         if (v <= r) pos += step;
       }
       const uint32_t j = pos - 1;
-      const uint32_t wbase = (uint32_t)__shfl((int)base_t, (int)j);
-      const uint32_t d = (uint32_t)__shfl((int)d_t, (int)j);
-      const uint64_t M = (uint64_t)__shfl((unsigned long long)m_t, (int)j);
-      const uint32_t c32 = (uint32_t)__shfl((int)c32_t, (int)j);
+      const uint4 sl = slots[wv][j];
+      const uint32_t wbase = sl.x, d = sl.y;
+      const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;
+      const uint32_t c32 = slot_c32[wv][j];
       const uint64_t s = kbase + oa0;
       const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
       // this round's chunks into LDS, then the next round's plan and loads
@@ -554,10 +569,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
         fetch_span(plan, ch0, ch1);
         oa0 = ob0;
         oa1 = ob1;
-        if (r + 128u < nkeys) {
-          ob0 = ko[r + 128];
-          ob1 = ko[r + 129];
-        }
+        if (r + 128u < nkeys) load_off2(ko, r + 128, ob0, ob1);
       }
       const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
       if (!act) continue;
