@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -26,20 +27,18 @@ bool host_pinned(const void* p) {
   return attr.type == hipMemoryTypeHost;
 }
 
-// ---- copy-thread pool: one job at a time, the caller works on it too ----
+// ---- worker pool: one job at a time, the caller works on it too ----
 namespace {
 
-class CopyPool {
+class WorkPool {
  public:
-  void run(void* dst, const void* src, size_t n) {
+  void run(size_t pieces, const std::function<void(size_t)>& fn) {
     std::lock_guard<std::mutex> job(job_mu_);
     start();
     {
       std::lock_guard<std::mutex> l(mu_);
-      dst_ = static_cast<char*>(dst);
-      src_ = static_cast<const char*>(src);
-      n_ = n;
-      pieces_ = (n + kPiece - 1) / kPiece;
+      fn_ = &fn;
+      pieces_ = pieces;
       next_ = finished_ = 0;
       gen_++;
     }
@@ -47,10 +46,10 @@ class CopyPool {
     work();
     std::unique_lock<std::mutex> l(mu_);
     done_cv_.wait(l, [&] { return finished_ == pieces_; });
+    fn_ = nullptr;
   }
 
  private:
-  static constexpr size_t kPiece = 1u << 20;
   void start() {
     if (!threads_.empty()) return;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -73,13 +72,14 @@ class CopyPool {
   void work() {
     for (;;) {
       size_t k;
+      const std::function<void(size_t)>* fn;
       {
         std::lock_guard<std::mutex> l(mu_);
         if (next_ >= pieces_) return;
         k = next_++;
+        fn = fn_;
       }
-      const size_t off = k * kPiece, len = std::min(kPiece, n_ - off);
-      memcpy(dst_ + off, src_ + off, len);
+      (*fn)(k);
       std::lock_guard<std::mutex> l(mu_);
       if (++finished_ == pieces_) done_cv_.notify_all();
     }
@@ -87,14 +87,13 @@ class CopyPool {
   std::mutex job_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> threads_;
-  char* dst_ = nullptr;
-  const char* src_ = nullptr;
-  size_t n_ = 0, pieces_ = 0, next_ = 0, finished_ = 0;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t pieces_ = 0, next_ = 0, finished_ = 0;
   uint64_t gen_ = 0;
 };
 
-CopyPool* pool() {
-  static CopyPool* p = new CopyPool;  // never destroyed: its threads outlive static teardown
+WorkPool* pool() {
+  static WorkPool* p = new WorkPool;  // never destroyed: its threads outlive static teardown
   return p;
 }
 
@@ -104,12 +103,26 @@ HostSession* g_sessions[kMaxDevices] = {};
 
 }  // namespace
 
+void parallel_for(size_t pieces, const std::function<void(size_t)>& fn) {
+  if (pieces == 1) {
+    fn(0);
+    return;
+  }
+  if (pieces > 1) pool()->run(pieces, fn);
+}
+
 void parallel_copy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPiece = 1u << 20;
   if (n < (4u << 20)) {
     memcpy(dst, src, n);
     return;
   }
-  pool()->run(dst, src, n);
+  char* d = static_cast<char*>(dst);
+  const char* s = static_cast<const char*>(src);
+  parallel_for((n + kPiece - 1) / kPiece, [&](size_t k) {
+    const size_t off = k * kPiece;
+    memcpy(d + off, s + off, std::min(kPiece, n - off));
+  });
 }
 
 // ---- buffers ----

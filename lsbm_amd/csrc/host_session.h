@@ -11,7 +11,7 @@
 // lsbm_crc32c_shutdown() frees everything.
 //
 // Copies into pinned memory are the host's share of the work: copies of 4 MiB
-// and more are split over a pool of copy threads so that the staging
+// and more are split over a pool of worker threads so that the staging
 // keeps up with PCIe (~55 GB/s measured for pinned H2D on the MI355X box).
 // A source that is already page-locked (hipHostMalloc / hipHostRegister) is
 // DMA-ed directly.  All DMA is stream-ordered hipMemcpyAsync on the stage's
@@ -23,6 +23,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
 #include <mutex>
 
 #include "../../include/lsbm/status.h"
@@ -132,7 +133,11 @@ class SessionLease {
 // Is p inside page-locked host memory (hipHostMalloc'd or registered)?
 bool host_pinned(const void* p);
 
-// memcpy of n bytes, split over the copy-thread pool when n >= 4 MiB.
+// fn(0) ... fn(pieces - 1) over the worker pool (15 threads and the caller),
+// one job at a time; returns when all have run.
+void parallel_for(size_t pieces, const std::function<void(size_t)>& fn);
+
+// memcpy of n bytes, split over the worker pool when n >= 4 MiB.
 void parallel_copy(void* dst, const void* src, size_t n);
 
 // Status for a failed HIP call.

@@ -1,8 +1,8 @@
 // log_checksum.cc -- include/lsbm/log_checksum.h on top of the C ABI.
 //
 // Writer side: framing on the host (it is a memcpy), every header CRC of a
-// batch in one lsbm_log_seal_dev launch.  Reader side: a first walk over the
-// image finds every header the reference reader could check, one
+// batch in one lsbm_log_seal_dev launch.  Reader side: a parallel walk over the
+// image's 32 KiB blocks finds every header the reference reader could check, one
 // lsbm_log_verify_dev launch checks them all, and a second walk replays
 // log::Reader::ReadRecord / ReadPhysicalRecord (common/log_reader.cc:59-256)
 // with those results, so records and Reporter calls come out in the
@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 
 #include "../../include/lsbm_crc32c.h"
 #include "host_session.h"
@@ -108,24 +109,38 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
 
 inline uint32_t header_length(const uint8_t* h) { return (uint32_t)h[4] | ((uint32_t)h[5] << 8); }
 
+// The headers log::Reader meets in one log block [b, e), every checksum
+// assumed good: ReadPhysicalRecord (common/log_reader.cc:179-256) hops from
+// header to header until fewer than kHeaderSize bytes are left, a length
+// reaches past the block ("bad record length") or a zero-type zero-length
+// record (preallocated space) ends the block.  Unknown types and records
+// before initial_offset are passed over, not ended at; a checksum mismatch
+// would drop the rest of the block, so the replay visits a subset of these.
+void block_headers(const uint8_t* f, uint64_t b, uint64_t e, std::vector<uint64_t>* out) {
+  while (e - b >= (uint64_t)kHeaderSize) {
+    const uint32_t length = header_length(f + b);
+    if (kHeaderSize + length > e - b) return;
+    if (f[b + 6] == kZeroType && length == 0) return;
+    out->push_back(b);
+    b += kHeaderSize + length;
+  }
+}
+
 // log::Reader's values beyond the record types (common/log_reader.h:77-85).
 // A type byte of 5 or 6 reads as one of them, exactly as in the reference.
 enum : unsigned int { kEof = kMaxRecordType + 1, kBadRecord = kMaxRecordType + 2 };
 
 }  // namespace
 
-// One pass of log::Reader over an in-memory file (checksum = true, any
-// initial_offset).  In the collecting pass every header whose checksum the
-// reader would test is recorded and assumed good; in the replay pass the
-// GPU's verdicts are used and Reporter calls are made.  The reader's buffer_
+// log::Reader over an in-memory file (checksum = true, any initial_offset),
+// with the GPU's checksum verdicts for the headers block_headers found.  The reader's buffer_
 // is file[buf_begin_, buf_end_) and buf_end_ is its end_of_buffer_offset_.
 class Walk {
  public:
   Walk(const uint8_t* file, size_t size, uint64_t initial_offset, Reporter* reporter,
-       std::vector<uint64_t>* collect, const std::vector<uint64_t>* checked,
-       const std::vector<uint8_t>* ok)
-      : file_(file), size_(size), reporter_(reporter), collect_(collect), checked_(checked),
-        ok_(ok), initial_offset_(initial_offset) {}
+       const std::vector<uint64_t>* checked, const std::vector<uint8_t>* ok)
+      : file_(file), size_(size), reporter_(reporter), checked_(checked), ok_(ok),
+        initial_offset_(initial_offset) {}
 
   // log::Reader::ReadRecord (common/log_reader.cc:59-162).
   bool ReadRecord(std::string* record, uint64_t* record_offset) {
@@ -267,10 +282,6 @@ class Walk {
   }
 
   bool ChecksumOk(uint64_t header) {
-    if (collect_) {
-      collect_->push_back(header);
-      return true;
-    }
     // the replay visits a subset of the collected headers, in order
     while (next_ < checked_->size() && (*checked_)[next_] < header) next_++;
     return next_ < checked_->size() && (*checked_)[next_] == header && (*ok_)[next_] != 0;
@@ -279,14 +290,13 @@ class Walk {
   // log::Reader::ReportDrop (common/log_reader.cc:171-176): drops that begin
   // before initial_offset_ are not reported (uint64 arithmetic, as there).
   void Report(size_t bytes, const char* reason) {
-    if (reporter_ && !collect_ && buf_begin_ - (uint64_t)bytes >= initial_offset_)
+    if (reporter_ && buf_begin_ - (uint64_t)bytes >= initial_offset_)
       reporter_->Corruption(bytes, Status::Corruption(reason));
   }
 
   const uint8_t* file_;
   size_t size_;
   Reporter* reporter_;
-  std::vector<uint64_t>* collect_;
   const std::vector<uint64_t>* checked_;
   const std::vector<uint8_t>* ok_;
   size_t next_ = 0;
@@ -330,14 +340,22 @@ Status BatchWriter::Seal(int device) {
   if (count == 0) return Status::OK();
   // the unsealed tail of the log: every pending header's masked crc (4 B each
   // come back), EncodeFixed32 into its header (util/coding.cc)
-  std::vector<uint32_t> masked(count);
+  std::unique_ptr<uint32_t[]> masked(new uint32_t[count]);
   Status s = run_log(device, dest_.data(), headers_[sealed_], dest_.size(), &headers_[sealed_],
-                     count, true, reinterpret_cast<uint8_t*>(masked.data()));
+                     count, true, reinterpret_cast<uint8_t*>(masked.get()));
   if (!s.ok()) return s;
-  for (size_t i = 0; i < count; i++) {
-    char* h = &dest_[headers_[sealed_ + i]];
-    for (int k = 0; k < 4; k++) h[k] = (char)(masked[i] >> (8 * k));
-  }
+  // EncodeFixed32 into each header; scattered 4-byte stores over the whole
+  // image, so split over the worker pool
+  constexpr size_t kPiece = 1u << 16;
+  char* img = &dest_[0];
+  const uint64_t* heads = &headers_[sealed_];
+  parallel_for((count + kPiece - 1) / kPiece, [&](size_t k) {
+    const size_t i1 = std::min(count, (k + 1) * kPiece);
+    for (size_t i = k * kPiece; i < i1; i++) {
+      char* h = img + heads[i];
+      for (int b = 0; b < 4; b++) h[b] = (char)(masked[i] >> (8 * b));
+    }
+  });
   sealed_ = headers_.size();
   return Status::OK();
 }
@@ -353,11 +371,30 @@ Status BatchReader::Verify(int device) {
   delete walk_;
   walk_ = nullptr;
   headers_.clear();
-  {  // pass 1: every header the reader could check (all checksums assumed good)
-    Walk collect(img, size_, initial_offset_, nullptr, &headers_, nullptr, nullptr);
-    std::string rec;
-    uint64_t off = 0;
-    while (collect.ReadRecord(&rec, &off)) {
+  {  // pass 1: every header the reader could check (all checksums assumed good).
+    // Records never cross a block (common/log_writer.cc:33-40) and the reader
+    // restarts at every block, so blocks are walked independently, in
+    // parallel: the reader's first block (log::Reader::SkipToInitialBlock,
+    // common/log_reader.cc:35-57) to the end of the file.
+    const uint64_t in_block = initial_offset_ % kBlockSize;
+    uint64_t first = initial_offset_ - in_block;
+    if (in_block > (uint64_t)kBlockSize - 6) first += kBlockSize;
+    if (first < size_) {
+      constexpr uint64_t kPieceBlocks = 64;  // 2 MiB of log per piece
+      const uint64_t blocks = (size_ - first + kBlockSize - 1) / kBlockSize;
+      const size_t pieces = (size_t)((blocks + kPieceBlocks - 1) / kPieceBlocks);
+      std::vector<std::vector<uint64_t>> part(pieces);
+      parallel_for(pieces, [&](size_t k) {
+        const uint64_t b0 = first + k * kPieceBlocks * kBlockSize;
+        const uint64_t b1 = std::min<uint64_t>(size_, b0 + kPieceBlocks * kBlockSize);
+        part[k].reserve((b1 - b0) / 512);
+        for (uint64_t b = b0; b < b1; b += kBlockSize)
+          block_headers(img, b, std::min<uint64_t>(b1, b + kBlockSize), &part[k]);
+      });
+      size_t total = 0;
+      for (const auto& v : part) total += v.size();
+      headers_.reserve(total);
+      for (const auto& v : part) headers_.insert(headers_.end(), v.begin(), v.end());
     }
   }
   ok_.assign(headers_.size(), 0);
@@ -366,7 +403,7 @@ Status BatchReader::Verify(int device) {
     if (!s.ok()) return s;
   }
   // pass 2 (ReadRecord): the reader itself, with the GPU's verdicts
-  walk_ = new Walk(img, size_, initial_offset_, reporter_, nullptr, &headers_, &ok_);
+  walk_ = new Walk(img, size_, initial_offset_, reporter_, &headers_, &ok_);
   return Status::OK();
 }
 

@@ -10,7 +10,8 @@
 // blocks with trailers, printable bytes); every sealed table is re-checked
 // on a sample of blocks against util/crc32c.h (the library's scalar API).
 //
-//   build: g++ -O2 -std=c++17 -Iinclude tools/bench_host_layers.cc -Llsbm_amd -llsbm_crc32c \
+//   build: g++ -O2 -std=c++17 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+//          tools/bench_host_layers.cc -Llsbm_amd -llsbm_crc32c \
 //          -Wl,-rpath,lsbm_amd -lamdhip64 -L/opt/rocm/lib -pthread -o build/bench_host_layers
 //   run:   build/bench_host_layers [tables=1000] [wal_mb=1024]
 #include <hip/hip_runtime_api.h>
@@ -99,16 +100,22 @@ int main(int argc, char** argv) {
   {
     const size_t n = 1u << 30;
     void *h = nullptr, *d = nullptr;
-    hipHostMalloc(&h, n, hipHostMallocDefault);
-    hipMalloc(&d, n);
+    if (hipHostMalloc(&h, n, hipHostMallocDefault) != hipSuccess || hipMalloc(&d, n) != hipSuccess) {
+      fprintf(stderr, "h2d ceiling: allocation failed\n");
+      return 1;
+    }
     memset(h, 1, n);
-    hipMemcpy(d, h, n, hipMemcpyHostToDevice);
+    bool ok = hipMemcpy(d, h, n, hipMemcpyHostToDevice) == hipSuccess;
     double t0 = now();
-    for (int r = 0; r < 3; r++) hipMemcpy(d, h, n, hipMemcpyHostToDevice);
+    for (int r = 0; r < 3; r++) ok = ok && hipMemcpy(d, h, n, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+      fprintf(stderr, "h2d ceiling: copy failed\n");
+      return 1;
+    }
     const double el = (now() - t0) / 3;
     printf("{\"what\": \"h2d_pinned_copy\", \"bytes\": %zu, \"GBps\": %.2f}\n", n, n / el / 1e9);
-    hipHostFree(h);
-    hipFree(d);
+    (void)hipHostFree(h);
+    (void)hipFree(d);
   }
   // ---- one 16 MiB table ----
   {
@@ -143,7 +150,11 @@ int main(int argc, char** argv) {
     }
     for (int pinned = 0; pinned < 2; pinned++) {
       if (pinned)
-        for (auto& t : ts) hipHostRegister(t.img.data(), t.img.size(), hipHostRegisterDefault);
+        for (auto& t : ts)
+          if (hipHostRegister(t.img.data(), t.img.size(), hipHostRegisterDefault) != hipSuccess) {
+            fprintf(stderr, "hipHostRegister failed\n");
+            return 1;
+          }
       lsbm::Status s = lsbm::SealTables(0, im.data(), 1);  // warm
       double t0 = now();
       s = lsbm::SealTables(0, im.data(), ntables);
@@ -162,7 +173,7 @@ int main(int argc, char** argv) {
              ntables, bytes, pinned, s.ToString().c_str(), el_s, bytes / el_s / 1e9, v.ToString().c_str(),
              el_v, bytes / el_v / 1e9, nok, ok.size(), bad);
       if (pinned)
-        for (auto& t : ts) hipHostUnregister(t.img.data());
+        for (auto& t : ts) (void)hipHostUnregister(t.img.data());
     }
   }
   // ---- a WAL: one group commit of ~wal_mb MiB, then recovery's read ----
