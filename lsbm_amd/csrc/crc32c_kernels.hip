@@ -236,20 +236,13 @@ constexpr uint64_t kLogHeaderSize = 7;  // common/log_format.h:30 (crc 4, length
 constexpr uint64_t kLogNoHeader = ~0ull;  // ExtRaw.y of a header that is not inside the image
 constexpr uint64_t kTrailer = 5;        // table/format.h:84 kBlockTrailerSize
 
+// Log headers: this loads the header offset only (r.x); log_length() adds the
+// record length, a load that depends on it (see crc32c_units_kernel).
 __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) {
   ExtRaw r = {0, 0};
   if (a.extents == kExtLogHeaders) {
-    // header offset, then the record length (LE16 at h + 4) read byte-wise;
-    // a header that does not fit the image reads the zero pad instead
     const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
     r.x = h[b];
-    const bool inside = r.x <= a.limit && a.limit - r.x >= kLogHeaderSize;
-    uint64_t p = inside ? reinterpret_cast<uint64_t>(a.base) + r.x + 4
-                        : reinterpret_cast<uint64_t>(a.dc->zero16);
-    asm volatile("" : "+v"(p));  // defined in every lane (see crc32c_units_kernel)
-    const gptr_u8 q = reinterpret_cast<gptr_u8>(p);
-    const uint64_t len = (uint64_t)q[0] | ((uint64_t)q[1] << 8);
-    r.y = inside ? len : kLogNoHeader;
   } else if (a.extents == kExtHandles) {
     const gptr_u64 h = reinterpret_cast<gptr_u64>(reinterpret_cast<uint64_t>(a.handles));
     r.x = h[2 * b];
@@ -260,6 +253,18 @@ __device__ __forceinline__ ExtRaw load_ext_raw(const RaggedArgs& a, uint64_t b) 
     r.y = o[b + 1];
   }
   return r;
+}
+
+// The record length (LE16 at header + 4, read byte-wise) into r.y; a header
+// that does not fit the image reads the zero pad instead and gets kLogNoHeader.
+__device__ __forceinline__ void log_length(const RaggedArgs& a, ExtRaw& r) {
+  const bool inside = r.x <= a.limit && a.limit - r.x >= kLogHeaderSize;
+  uint64_t p = inside ? reinterpret_cast<uint64_t>(a.base) + r.x + 4
+                      : reinterpret_cast<uint64_t>(a.dc->zero16);
+  asm volatile("" : "+v"(p));  // defined in every lane (see crc32c_units_kernel)
+  const gptr_u8 q = reinterpret_cast<gptr_u8>(p);
+  const uint64_t len = (uint64_t)q[0] | ((uint64_t)q[1] << 8);
+  r.y = inside ? len : kLogNoHeader;
 }
 
 // Block b's extent [s, e) as absolute addresses, whether the record fits the
@@ -469,6 +474,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   // records are near-uniform)
   uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
 #ifndef LSBM_NO_BALANCE  // A/B builds only
+  // (log records too by bytes, keyed on header offsets: 3 points slower on a
+  // 0.5 GB WAL, the search's latency costs more than the uneven counts;
+  // profiles/r02/ab/s56_log_byte_ranges.log)
   if constexpr ((kMode == kModeOut || kMode == kModeVerify) &&
                 (kExt == kExtOffsets || kExt == kExtHandles))
     if (args.n >= 16u * nwaves) byte_ranges<kExt>(args, wave, nwaves, b_lo, b_hi);
@@ -493,6 +501,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   uint32_t ivj = 0;
   if (b_lo < b_hi) prefetch(cur_b, rj, ivj);
   load_lds_tables(g_lds, dc);  // overlaps the first extents' latency
+  if constexpr (kExt == kExtLogHeaders) log_length(args, rj);
 
   // The block still open at the end of the last retired round and the xor of
   // its units so far (wave-uniform); ~0 = none.
@@ -824,6 +833,12 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     absorb_start(ba[1], 1);
     absorb(ba[2], 2);
     absorb(ba[3], 3);
+    // Log headers: the next round's record lengths.  Their header offsets were
+    // loaded before this round's first row bank, so they have landed by now
+    // (vmcnt retires in order); issued right behind the offsets, the dependent
+    // load made every round wait out a memory latency with no row loads in
+    // flight (A/B: +1.2 points on every log mode, profiles/r02/ab/s55_*).
+    if constexpr (kExt == kExtLogHeaders) log_length(args, rn);
     // End fix.  The register kept per braid is the pre-lookup word c = s ^ w
     // of the last row absorbed, and the row loop absorbed w = 0 for the chunk
     // straddling e, so adding its bytes < e is a plain xor after the loop:

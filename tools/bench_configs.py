@@ -336,6 +336,8 @@ def wal(args):
     from lsbm_amd._lib import lib
     rng = np.random.default_rng(0xA1)
     lens = rng.integers(0, 2541, size=args.wal_records)
+    if args.wal_fixed_len is not None:  # (diagnostic: no length spread)
+        lens[:] = args.wal_fixed_len
     pay = printable_bytes(0xA2, int(lens.sum()))
     offs = np.concatenate([[0], np.cumsum(lens)])
     wimg, heads = log.layout_records(pay[offs[i]:offs[i + 1]] for i in range(lens.size))
@@ -358,6 +360,10 @@ def wal(args):
     torch.cuda.synchronize()
     img = d.cpu().numpy()
     plen = img[heads + 4].astype(np.int64) | (img[heads + 5].astype(np.int64) << 8)
+    # (diagnostic) the same bytes as {offset, length} extents: no header load
+    ext = torch.from_numpy(np.stack([heads.astype(np.int64) + 6, plen + 1], 1).reshape(-1)).to("cuda")
+    ep = ctypes.c_void_p(ext.data_ptr())
+    t_ext = time_launches(lambda: L.lsbm_crc32c_extents_dev(dp, ep, n, None, mp, 0, sp), s)
     crc_bytes = int(plen.sum()) + n
     o = oracle()
     bad = 0
@@ -366,12 +372,13 @@ def wal(args):
         want = o.mask(o.value(img[h + 6:h + 7 + int(plen[i])].tobytes()))
         bad += int(want != int.from_bytes(img[h:h + 4].tobytes(), "little"))
     pct = lambda t: round(crc_bytes / t / 1e9 / HBM * 100, 2)
-    print(json.dumps({"config": "wal", "records": int(lens.size), "physical": int(n), "crc_bytes": crc_bytes,
+    print(json.dumps({"config": "wal", "fixed_len": args.wal_fixed_len, "records": int(lens.size), "physical": int(n), "crc_bytes": crc_bytes,
                       "log_seal": {"ms": round(t_seal * 1e3, 3), "pct_hbm_peak": pct(t_seal)},
                       "log_seal_no_out": {"ms": round(t_seal_nm * 1e3, 3), "pct_hbm_peak": pct(t_seal_nm)},
                       "log_crcs": {"ms": round(t_crcs * 1e3, 3), "pct_hbm_peak": pct(t_crcs)},
                       "log_verify": {"ms": round(t_ver * 1e3, 3), "pct_hbm_peak": pct(t_ver),
                                      "all_ok": bool(ok.all().item())},
+                      "extents_same_bytes": {"ms": round(t_ext * 1e3, 3), "pct_hbm_peak": pct(t_ext)},
                       "sample_mismatches": bad}), flush=True)
 
 
@@ -383,6 +390,7 @@ def main():
     p.add_argument("--host-blocks", type=int, default=1 << 18)
     p.add_argument("--sst-blocks", type=int, default=1 << 20)
     p.add_argument("--wal-records", type=int, default=400_000)
+    p.add_argument("--wal-fixed-len", type=int, default=None)
     args = p.parse_args()
     import torch
     torch.cuda.set_device(0)
