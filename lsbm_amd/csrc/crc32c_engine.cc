@@ -31,6 +31,8 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
                         const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
                         const DevConsts* dc, int grid, hipStream_t stream);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
+hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint64_t* bounds, int grid,
+                               hipStream_t stream);
 hipError_t launch_trailer_scatter(uint8_t* file, uint64_t limit, const uint64_t* handles, const uint8_t* types,
                                   const uint32_t* crcs, uint64_t n, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* buf, uint64_t nbytes, uint64_t seed, int grid, hipStream_t stream);
@@ -195,7 +197,14 @@ uint32_t u_noinit() {
   return u;
 }
 
-// One launch, no allocation, no host sync: graph-capturable like the fixed path.
+// One launch, no host sync.  A general batch (Out / Verify over offsets or
+// extents) of at least kMinChunks chunks of kChunkBlocks blocks per wave is
+// swept chunk by chunk (crc32c_units_kernel): a first small launch finds every
+// wave's byte-balanced range in every chunk, into (nchunks * nwaves + 1) * 8
+// bytes of stream-ordered scratch from the device's default pool (which
+// lsbm_crc32c_init sets to keep freed memory).  Without that scratch, and
+// while the stream is being captured into a graph, the batch goes as one
+// range per wave.
 int run_ragged(RaggedArgs a, hipStream_t stream) {
   DeviceState* st = nullptr;
   int rc = current_device(&st);
@@ -203,7 +212,38 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
   if (a.n == 0) return LSBM_OK;
   a.dc = st->d_consts;
   a.u_noinit = u_noinit();
+  a.bounds = nullptr;
+  a.nchunks = 0;
+  const uint64_t nwaves = (uint64_t)st->num_cus * kWavesPerWg;
+  // (LSBM_SWEEP_CHUNK_BLOCKS: A/B runs only; 0 = no chunked sweep)
+  static const uint64_t chunk_blocks = [] {
+    const char* v = getenv("LSBM_SWEEP_CHUNK_BLOCKS");
+    return v ? strtoull(v, nullptr, 10) : (uint64_t)kChunkBlocks;
+  }();
+  uint64_t* bounds = nullptr;
+  if (chunk_blocks > 0 && (a.mode == kModeOut || a.mode == kModeVerify) &&
+      (a.extents == kExtOffsets || a.extents == kExtHandles) &&
+      a.n >= (uint64_t)kMinChunks * chunk_blocks * nwaves && a.n < 0xffffffffull) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const uint64_t nchunks = a.n / (chunk_blocks * nwaves);
+    const uint64_t P = nchunks * nwaves;
+    if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
+        hipMallocAsync(reinterpret_cast<void**>(&bounds), (P + 1) * sizeof(uint64_t), stream) ==
+            hipSuccess) {
+      const hipError_t e = launch_range_bounds(a, P, bounds, (int)st->num_cus * 8, stream);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(bounds, stream);
+        return fail_hip(e, "range_bounds_kernel");
+      }
+      a.bounds = bounds;
+      a.nchunks = nchunks;
+    } else {
+      (void)hipGetLastError();  // (no scratch: one range per wave)
+      bounds = nullptr;
+    }
+  }
   const hipError_t e = launch_ragged(a, (int)st->num_cus, stream);
+  if (bounds) (void)hipFreeAsync(bounds, stream);
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_units_kernel");
 }
 

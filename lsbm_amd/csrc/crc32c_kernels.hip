@@ -391,27 +391,29 @@ __device__ __forceinline__ uint64_t start_key(const RaggedArgs& a, uint64_t b) {
   }
 }
 
-// Byte-balanced wave ranges.  With block lengths drawn from a skewed
-// distribution, equal block COUNTS per wave leave the heaviest wave ~9% above
-// the mean (10M Zipf blocks over 4,096 waves), and the kernel waits for it.
-// Wave w's range is [f(w), f(w + 1)) with f(w) the first block whose start is
-// at or past key(0) + (key(n) - key(0)) w / nwaves.  Both ends are found
-// together, lanes 0-31 for f(w) and 32-63 for f(w + 1), by a 32-ary search
-// (one load per lane per step, ~5 steps for 10M blocks).  The search only
-// ever compares key(p) >= t, so its result is non-decreasing in t for ANY
-// key array: the ranges tile [0, n) exactly even for an unsorted batch (which
-// is then merely not balanced).
+// Byte-balanced ranges.  With block lengths drawn from a skewed distribution,
+// equal block COUNTS per wave leave the heaviest wave ~9% above the mean (10M
+// Zipf blocks over 4,096 waves), and the kernel waits for it.  The batch is
+// cut into P pieces (one per wave, or one per wave and chunk); piece w is
+// [f(w), f(w + 1)) with f(w) the first block whose start is at or past
+// key(0) + (key(n) - key(0)) w / P.  Both ends are found together, lanes 0-31
+// for f(w) and 32-63 for f(w + 1), by a 32-ary search (one load per lane per
+// step, ~5 steps for 10M blocks).  The search only ever compares key(p) >= t,
+// so its result is non-decreasing in t for ANY key array: the pieces tile
+// [0, n) exactly even for an unsorted batch (which is then merely not
+// balanced).  P < 2^32.
 template <uint32_t kExt>
-__device__ __forceinline__ void byte_ranges(const RaggedArgs& a, uint64_t wave, uint64_t nwaves,
+__device__ __forceinline__ void byte_ranges(const RaggedArgs& a, uint64_t wave, uint64_t P,
                                             uint64_t& b_lo, uint64_t& b_hi) {
   const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, k = lane & 31u;
   const uint64_t k0 = start_key<kExt>(a, 0), kn = start_key<kExt>(a, a.n);
   if (kn <= k0) return;  // (wave-uniform) keep the equal counts
   const uint64_t w = wave + half;
-  const uint64_t t = k0 + (kn - k0) * w / nwaves;  // (kn - k0 < 2^50 bytes)
+  const uint64_t D = kn - k0;
+  const uint64_t t = k0 + (D / P) * w + ((D % P) * w) / P;  // k0 + floor(D w / P), no overflow
   // the answer lies in [lo, hi]; hi when no key in [lo, hi) reaches t.
-  // f(0) = 0 and f(nwaves) = n.
-  uint64_t lo = w >= nwaves ? a.n : 0, hi = w == 0 ? 0 : a.n;
+  // f(0) = 0 and f(P) = n.
+  uint64_t lo = w >= P ? a.n : 0, hi = w == 0 ? 0 : a.n;
   for (;;) {
     if (__ballot(hi - lo > 32u) == 0ull) break;
     const uint64_t step = (hi - lo + 31u) >> 5;
@@ -442,6 +444,21 @@ __device__ __forceinline__ void byte_ranges(const RaggedArgs& a, uint64_t wave, 
   b_hi = read64(f, 32);
 }
 
+// The chunked sweep's ranges: bounds[i] = f(i) for i in [0, P] (byte_ranges
+// with P pieces), one wave per two of them.
+template <uint32_t kExt>
+__global__ __launch_bounds__(256) void range_bounds_kernel(RaggedArgs args, uint64_t P, uint64_t* bounds) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = (uint64_t)gridDim.x * 4u;
+  for (uint64_t q = (uint64_t)blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+       2 * q <= P; q += nw) {
+    uint64_t lo = args.n * (2 * q) / P, hi = 2 * q + 1 <= P ? args.n * (2 * q + 1) / P : args.n;
+    byte_ranges<kExt>(args, 2 * q, P, lo, hi);
+    if (lane == 0) bounds[2 * q] = lo;
+    if (lane == 32 && 2 * q + 1 <= P) bounds[2 * q + 1] = hi;
+  }
+}
+
 // Units kernel.  Each wave owns a contiguous range of blocks and walks it in
 // rounds of 8 units (one per lane group).  The loop is software-pipelined so
 // that no global-memory latency is exposed between rounds:
@@ -469,24 +486,53 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
-  // this wave's contiguous range of blocks: equal counts, or equal bytes for
-  // general batches (whose lengths may be skewed; SSTable blocks and log
-  // records are near-uniform)
+  // This wave's blocks.  Big general batches are swept in chunks (args.bounds,
+  // from range_bounds_kernel): the batch is cut into nchunks chunks of about
+  // kChunkBlocks * nwaves blocks, each chunk into nwaves byte-balanced
+  // ranges, and wave w walks its range of every chunk in turn, so that all
+  // waves move through the batch together, one chunk at a time (128 blocks per
+  // wave: 6.5 GB of config 4's blocks; A/B 32 / 64 / 128 / 256 blocks,
+  // profiles/r02/ab/s62_s63_sweep_chunks.log: 128 and 256 best, +1.5-2 points
+  // on config 4, +2-3 on 117 GiB of equal 12 KiB blocks).
+  // With one contiguous range per wave, the waves' streams spread over the
+  // whole batch and the rate fell with its size: 81% of HBM peak for 16 GiB
+  // of equal 12 KiB blocks, 78% for 64 GiB, 75% for 117 GiB, and 78% for the
+  // 117 GiB as 7 separate launches (profiles/r02/ab/s58_usweep_size.log,
+  // s61_size_effect.log).  Range ends are block ends, so no block's units
+  // straddle two ranges.  (n < 2^32 - 1 there: round keys are 32-bit block
+  // indices relative to the wave's first block.)  Other batches: one range
+  // per wave, equal counts, or equal bytes for general batches (whose lengths
+  // may be skewed; SSTable blocks and log records are near-uniform).
+  const uint64_t* __restrict__ bnd = args.bounds;
+  const bool chunked = bnd != nullptr;
+  const uint64_t nchunks = args.nchunks;
   uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
+  uint64_t ck = 0;                      // the chunk being walked
+  uint64_t pf_lo = 0, pf_hi = 0;        // chunk ck + 1's range, loaded a chunk ahead
+  auto chunk_bounds = [&](uint64_t c, uint64_t& lo, uint64_t& hi) {  // c < nchunks
+    lo = bnd[c * nwaves + wave];
+    hi = bnd[c * nwaves + wave + 1];
+  };
+  if (chunked) {
+    chunk_bounds(0, b_lo, b_hi);
+    while (b_lo >= b_hi && ck + 1 < nchunks) chunk_bounds(++ck, b_lo, b_hi);  // (empty ranges)
+    if (ck + 1 < nchunks) chunk_bounds(ck + 1, pf_lo, pf_hi);
+  } else {
 #ifndef LSBM_NO_BALANCE  // A/B builds only
-  // (log records too by bytes, keyed on header offsets: 3 points slower on a
-  // 0.5 GB WAL, the search's latency costs more than the uneven counts;
-  // profiles/r02/ab/s56_log_byte_ranges.log)
-  if constexpr ((kMode == kModeOut || kMode == kModeVerify) &&
-                (kExt == kExtOffsets || kExt == kExtHandles))
-    if (args.n >= 16u * nwaves) byte_ranges<kExt>(args, wave, nwaves, b_lo, b_hi);
+    // (log records too by bytes, keyed on header offsets: 3 points slower on a
+    // 0.5 GB WAL, the search's latency costs more than the uneven counts;
+    // profiles/r02/ab/s56_log_byte_ranges.log)
+    if constexpr ((kMode == kModeOut || kMode == kModeVerify) &&
+                  (kExt == kExtOffsets || kExt == kExtHandles))
+      if (args.n >= 16u * nwaves) byte_ranges<kExt>(args, wave, nwaves, b_lo, b_hi);
 #endif
+  }
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const uint32_t* __restrict__ init = args.init;
   constexpr uint32_t mode = kMode;
   const uint32_t jl = lane < 8u ? lane : 8u;  // lanes 0..8 hold the walk's 9 blocks
   // extents (+ init) of blocks nb + jl, clamped into the batch so that the
-  // loads are unconditional; only lanes with nb + lane < b_hi walk them
+  // loads are unconditional; only lanes with nb + lane < range_hi walk them
   auto prefetch = [&](uint64_t nb, ExtRaw& r, uint32_t& iv) {
     uint64_t idx = nb + jl;
     idx = idx < args.n ? idx : args.n - 1;
@@ -497,6 +543,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   // wave cursor: unit ordinal `cur_o` of block `cur_b` is the next unassigned unit
   uint64_t cur_b = b_lo;
   uint32_t cur_o = 0;
+  uint64_t range_hi = b_hi;  // end of the range being walked
   ExtRaw rj = {0, 0};
   uint32_t ivj = 0;
   if (b_lo < b_hi) prefetch(cur_b, rj, ivj);
@@ -524,7 +571,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       v = cols_apply(pshift, raw, li);  // A^(128 (k mod 512))
       if (pk >= kShiftCols) v = shift_rows(g_lds, dc, v, pk & ~(uint64_t)(kShiftCols - 1));
       v = pact ? v : 0u;
-      const uint32_t key = pact ? (uint32_t)(pb - b_lo) : ~0u;  // a range is < 2^32 blocks
+      const uint32_t key = pact ? (uint32_t)(pb - b_lo) : ~0u;  // a wave's blocks span < 2^32
       // segmented inclusive xor-scan over the 8 groups (blocks non-decreasing in g)
 #pragma unroll
       for (uint32_t d = 8; d < 64; d <<= 1) {
@@ -634,7 +681,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     pend_a = 0;
   };
 
-  while (cur_b < b_hi) {
+  while (cur_b < range_hi) {
     // Find the 8 groups' units in one round: lane j holds block cur_b + j
     // (8 units never span more than 9 blocks), an inclusive prefix sum over
     // the lanes' unit counts, then one ballot per group.  ALU + shuffles only:
@@ -643,7 +690,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     bool fj = true;
     extent_from_raw(args, cur_b + lane, rj, sj, ej, fj, atj);
     const Frame ft = frame_of(sj, ej, kMaxRows);
-    const bool vj = lane < 9u && cur_b + lane < b_hi;
+    const bool vj = lane < 9u && cur_b + lane < range_hi;
     const uint32_t units_j = vj ? ft.units : 0u;
     // Fast round: the cursor is at a block start and the next 8 blocks are
     // one unit each, so group g takes block cur_b + g (every round over an
@@ -676,7 +723,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     }
     const uint32_t my_t = cur_o + g;  // this group's unit, as an offset from the cursor
     const uint64_t b = cur_b + jg;
-    const bool active = jg < 9 && b < b_hi;
+    const bool active = jg < 9 && b < range_hi;
     Frame f = {0, 0, 0, 1, 1, 1, 0};
     f.s = __shfl((unsigned long long)ft.s, (int)jg);
     f.e = __shfl((unsigned long long)ft.e, (int)jg);
@@ -690,8 +737,21 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint64_t at = __shfl((unsigned long long)atj, (int)jg);
     const uint32_t o = my_t - pre_before;
     // the cursor after these 8 units, and the next round's extents
-    const uint64_t nb = cur_b + jnext;
-    const uint32_t no = cur_o + 8 - pre8;
+    uint64_t nb = cur_b + jnext;
+    uint32_t no = cur_o + 8 - pre8;
+    uint64_t next_hi = range_hi;
+    if (chunked && nb >= range_hi) {  // (wave-uniform) this range is done: the next chunk's
+      if (ck + 1 < nchunks) {
+        ck++;
+        nb = pf_lo;
+        next_hi = pf_hi;
+        while (nb >= next_hi && ck + 1 < nchunks) chunk_bounds(++ck, nb, next_hi);
+        if (ck + 1 < nchunks) chunk_bounds(ck + 1, pf_lo, pf_hi);
+      } else {
+        nb = next_hi = range_hi;  // (the last chunk: done)
+      }
+      no = 0;
+    }
     ExtRaw rn;
     uint32_t ivn;
     prefetch(nb, rn, ivn);
@@ -760,7 +820,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     const uint32_t fin_i = active ? (mode == kModeSstSeal || mode == kModeSstCrc ? 128u : 127u) - zf : 127u;
     const uint32_t st_i = (active ? (uint32_t)(k & (kShiftCols - 1)) : 0u) | (fin_i << 16) |
                           (last ? 1u << 24 : 0u) | (fits ? 1u << 25 : 0u) | (active ? 1u << 26 : 0u);
-    const uint32_t b_rel = (uint32_t)(b - b_lo);  // a wave's range is < 2^32 blocks
+    const uint32_t b_rel = (uint32_t)(b - b_lo);  // a wave's blocks span < 2^32
     const uint32_t k_hi = (uint32_t)(k >> 9);     // shift beyond the columns (blocks > 64 KiB)
 
     // uniform trip count: the longest unit of the 8 groups
@@ -910,6 +970,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     ivj = ivn;
     cur_b = nb;
     cur_o = no;
+    range_hi = next_hi;
   }
   retire();
   flush_stores();
@@ -1074,6 +1135,19 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
     else LSBM_LAUNCH_FIXED(false, 0);
   }
 #undef LSBM_LAUNCH_FIXED
+  return hipGetLastError();
+}
+
+hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint64_t* bounds, int grid,
+                               hipStream_t stream) {
+  const uint64_t want = (P / 2 + 1 + 3) / 4;  // 4 waves per workgroup, two bounds per wave
+  const dim3 g((unsigned)(want < (uint64_t)grid ? want : grid));
+  if (a.extents == kExtOffsets)
+    hipLaunchKernelGGL(range_bounds_kernel<kExtOffsets>, g, dim3(256), 0, stream, a, P, bounds);
+  else if (a.extents == kExtHandles)
+    hipLaunchKernelGGL(range_bounds_kernel<kExtHandles>, g, dim3(256), 0, stream, a, P, bounds);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

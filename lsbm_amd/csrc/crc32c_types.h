@@ -73,6 +73,13 @@ enum RaggedMode : uint32_t {
 // A^(128 k), k = the frame's rows after the unit; the units of a block are
 // summed inside the wave (crc32c_kernels.hip) and the block is finished by the
 // lane group holding its last unit.
+#ifndef LSBM_CHUNK_BLOCKS  // (A/B builds override; 0 = one contiguous range per wave)
+#define LSBM_CHUNK_BLOCKS 128
+#endif
+// Mean blocks per wave per chunk of the units kernel's chunked sweep, and the
+// fewest chunks a batch must make to be swept that way (crc32c_kernels.hip).
+constexpr uint32_t kChunkBlocks = LSBM_CHUNK_BLOCKS;
+constexpr uint32_t kMinChunks = 8;
 constexpr uint32_t kUnitRows = 48;  // A/B 24..96 rows: plateau from 48
 constexpr uint32_t kSstUnitRows = 40;  // SSTable trailer modes: a ~4 KiB block is one unit
 
@@ -96,6 +103,11 @@ struct RaggedArgs {
   uint32_t u_noinit;     // A^-4(~0): the virtual init bytes when init == nullptr
   uint64_t limit;        // kExtLogHeaders / SST modes: image size; records past it are
                          // empty + bad (~0 = unbounded)
+  // Chunked sweep (general Out / Verify batches of >= 8 chunks): wave w's
+  // range in chunk c is [bounds[c * nwaves + w], bounds[c * nwaves + w + 1]),
+  // c < nchunks, from range_bounds_kernel; null: one range per wave.
+  const uint64_t* bounds;
+  uint64_t nchunks;
 };
 
 }  // namespace lsbm

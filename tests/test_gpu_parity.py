@@ -6,6 +6,8 @@ full-size benchmark configs are checked on sampled blocks plus
 size-independent properties (two independent kernels agree on every block;
 known golden blocks of each config buffer).
 """
+import functools
+
 import numpy as np
 import pytest
 
@@ -160,6 +162,54 @@ def test_ragged_byte_balanced_ranges_skewed(torch_cuda, oracle, kind):
         ok, nbad = engine.crc32c_verify(d, _dev(torch, offs), _dev(torch, exp, torch.int32),
                                         masked=True)
         assert int(nbad.item()) == 97  # each block checked exactly once
+        assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(flip.tolist())
+        return
+    assert np.array_equal(got, want)
+
+
+_CHUNKED_N = 8 * 128 * 4096 + 12289  # kMinChunks x kChunkBlocks x 4,096 waves, and a partial
+
+
+@functools.lru_cache(maxsize=1)
+def _chunked_case():
+    n = _CHUNKED_N
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 100, size=n)
+    big = rng.random(n) < 0.0005
+    lens[big] = rng.integers(10_000, 100_000, size=int(big.sum()))
+    offs = (np.concatenate([[0], np.cumsum(lens)]) + 3).astype(np.int64)
+    return lens, offs, stream_bytes(n, 0, int(offs[-1]) + 64)
+
+
+@pytest.mark.parametrize("kind", ["offsets", "extents_shuffled", "verify"])
+def test_ragged_chunked_sweep_exact(torch_cuda, oracle, kind):
+    """General batches of >= 8 chunks of 128 blocks per wave are swept chunk
+    by chunk, each chunk cut into byte-balanced ranges by range_bounds_kernel
+    (crc32c_engine.cc run_ragged).  Blocks of 10-100 KB among 0-100-B ones
+    span several ranges' worth of bytes, so some ranges are empty (a wave's
+    first one included); with shuffled extents the starts are unsorted and the
+    ranges merely unbalanced.  Every block computed once and right."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n = _CHUNKED_N
+    lens, offs, data = _chunked_case()
+    want = oracle.batch_offsets(data, offs.astype(np.uint64), None, kind == "verify")
+    d = _dev(torch, data)
+    rng = np.random.default_rng(7)
+    if kind == "offsets":
+        got = _u32(engine.crc32c_batch(d, _dev(torch, offs)))
+    elif kind == "extents_shuffled":
+        order = rng.permutation(n)
+        ext = np.stack([offs[:-1][order], lens[order]], 1).reshape(-1).astype(np.int64)
+        got = np.empty(n, dtype=np.uint32)
+        got[order] = _u32(engine.crc32c_extents(d, _dev(torch, ext)))
+    else:
+        exp = want.copy()
+        flip = rng.choice(n, size=131, replace=False)
+        exp[flip] ^= 0x4
+        ok, nbad = engine.crc32c_verify(d, _dev(torch, offs), _dev(torch, exp, torch.int32),
+                                        masked=True)
+        assert int(nbad.item()) == 131  # each block checked exactly once
         assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(flip.tolist())
         return
     assert np.array_equal(got, want)
@@ -625,7 +675,8 @@ def test_sst_handles_past_the_image(torch_cuda, oracle):
 
 
 @pytest.mark.parametrize("seed,smax,n", [(31, 130, 20000), (32, 70, 20000), (33, 5000, 20000),
-                                         (34, 130, 150000), (35, 12, 150000)])
+                                         (34, 130, 150000), (35, 12, 150000),
+                                         (36, 130, 600000), (37, 12, 1100000)])
 def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax, n):
     """Every trailer of a table whose blocks are 0..smax bytes: all trailers
     and every byte between and after them must come out exactly right.  From

@@ -143,6 +143,25 @@ def c4uniform(args):
     del d, do
 
 
+def usweep(args):
+    """(diagnostic) equal-length blocks through the ragged kernel, 16 GiB per
+    length, 5 bytes off alignment: the per-round cost against the unit count."""
+    import torch
+    from lsbm_amd import engine
+    total = args.sweep_gib << 30
+    d = torch.empty(total + 4096, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 0x5EED0003)
+    s = torch.cuda.current_stream()
+    for L in args.sweep_lens:
+        n = total // L
+        do = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device="cuda") + 5
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        t = time_launches(lambda: engine.crc32c_batch(d, do, out=out, stream=s), s, reps=5, warm=1)
+        print(json.dumps({"config": "usweep", "len": L, "blocks": n, "ms": round(t * 1e3, 3),
+                          "pct_hbm_peak": round(100 * n * L / t / 1e9 / HBM, 2)}), flush=True)
+    del d
+
+
 def config4(args):
     import torch
     from lsbm_amd import engine
@@ -391,13 +410,16 @@ def main():
     p.add_argument("--sst-blocks", type=int, default=1 << 20)
     p.add_argument("--wal-records", type=int, default=400_000)
     p.add_argument("--wal-fixed-len", type=int, default=None)
+    p.add_argument("--sweep-gib", type=int, default=16)
+    p.add_argument("--sweep-lens", type=int, nargs="+",
+                   default=[1024, 2048, 4096, 6144, 8192, 12288, 16384, 24576, 49152, 65536])
     args = p.parse_args()
     import torch
     torch.cuda.set_device(0)
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "config1": config1, "config3": config3, "config4": config4, "host": host_staged,
+        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "usweep": usweep, "config1": config1, "config3": config3, "config4": config4, "host": host_staged,
          "wal": wal}[w](args)
 
 
