@@ -169,7 +169,9 @@ def main():
     n = args.blocks
     # the CPU baseline first, in forked worker processes, before this process
     # touches the GPU (no child ever holds a device context)
-    cpu = cpu_baselines(buf, offs_h, min(n, args.cpu_sample), args.cpu_seconds)
+    # (--cpu-seconds 0: no CPU baseline, e.g. under rocprofv3 --pmc, whose
+    # library has initialised the GPU before this process could fork)
+    cpu = cpu_baselines(buf, offs_h, min(n, args.cpu_sample), args.cpu_seconds) if args.cpu_seconds > 0 else {}
     import torch
     from lsbm_amd import engine, snappy
     engine.init(0)

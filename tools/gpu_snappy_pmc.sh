@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/spmc
-CMD="python3 tools/bench_snappy.py --reps 3 --cpu-seconds 0.5"
+CMD="python3 tools/bench_snappy.py --reps 3 --cpu-seconds 0"
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/spmc/stats -o run -- $CMD > gpurun_out/spmc/stats.log 2>&1
 rc=$?; echo "stats rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/spmc/stats.log; exit $rc; }
 i=0
