@@ -79,7 +79,13 @@ int lsbm_crc32c_fixed_dev(const void* d_base, uint64_t stride, uint64_t len, uin
                           const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
 
 /* Ragged batch: block i = d_base[offsets[i], offsets[i+1]) (d_offsets has
- * n_blocks+1 entries, non-decreasing not required; any alignment). */
+ * n_blocks+1 entries, non-decreasing not required; any alignment).
+ * Big batches (this, extents and verify; from 8 x 128 blocks per wave of the
+ * device, 4.2M blocks on an MI355X) are swept chunk by chunk: a first small
+ * launch on the stream writes the chunks' ranges into ~n_blocks / 16 bytes
+ * of stream-ordered scratch (hipMallocAsync from the device's default pool,
+ * freed on the stream after the CRC launch).  Without it, or while the
+ * stream is being captured, one launch as for smaller batches. */
 int lsbm_crc32c_batch_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n_blocks,
                           const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream);
 
