@@ -82,7 +82,7 @@ int lsbm_crc32c_fixed_dev(const void* d_base, uint64_t stride, uint64_t len, uin
  * n_blocks+1 entries, non-decreasing not required; any alignment).
  * Big batches (this, extents and verify; from 8 x 128 blocks per wave of the
  * device, 4.2M blocks on an MI355X) are swept chunk by chunk: a first small
- * launch on the stream writes the chunks' ranges into ~n_blocks / 16 bytes
+ * launch on the stream writes the chunks' ranges into ~n_blocks / 32 bytes
  * of stream-ordered scratch (hipMallocAsync from the device's default pool,
  * freed on the stream after the CRC launch).  Without it, or while the
  * stream is being captured, one launch as for smaller batches. */

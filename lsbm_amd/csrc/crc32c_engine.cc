@@ -31,7 +31,7 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
                         const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
                         const DevConsts* dc, int grid, hipStream_t stream);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
-hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint64_t* bounds, int grid,
+hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint32_t* bounds, int grid,
                                hipStream_t stream);
 hipError_t launch_trailer_scatter(uint8_t* file, uint64_t limit, const uint64_t* handles, const uint8_t* types,
                                   const uint32_t* crcs, uint64_t n, int grid, hipStream_t stream);
@@ -200,7 +200,7 @@ uint32_t u_noinit() {
 // One launch, no host sync.  A general batch (Out / Verify over offsets or
 // extents) of at least kMinChunks chunks of kChunkBlocks blocks per wave is
 // swept chunk by chunk (crc32c_units_kernel): a first small launch finds every
-// wave's byte-balanced range in every chunk, into (nchunks * nwaves + 1) * 8
+// wave's byte-balanced range in every chunk, into (nchunks * nwaves + 1) * 4
 // bytes of stream-ordered scratch from the device's default pool (which
 // lsbm_crc32c_init sets to keep freed memory).  Without that scratch, and
 // while the stream is being captured into a graph, the batch goes as one
@@ -220,7 +220,7 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
     const char* v = getenv("LSBM_SWEEP_CHUNK_BLOCKS");
     return v ? strtoull(v, nullptr, 10) : (uint64_t)kChunkBlocks;
   }();
-  uint64_t* bounds = nullptr;
+  uint32_t* bounds = nullptr;
   if (chunk_blocks > 0 && (a.mode == kModeOut || a.mode == kModeVerify) &&
       (a.extents == kExtOffsets || a.extents == kExtHandles) &&
       a.n >= (uint64_t)kMinChunks * chunk_blocks * nwaves && a.n < 0xffffffffull) {
@@ -228,7 +228,7 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
     const uint64_t nchunks = a.n / (chunk_blocks * nwaves);
     const uint64_t P = nchunks * nwaves;
     if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
-        hipMallocAsync(reinterpret_cast<void**>(&bounds), (P + 1) * sizeof(uint64_t), stream) ==
+        hipMallocAsync(reinterpret_cast<void**>(&bounds), (P + 1) * sizeof(uint32_t), stream) ==
             hipSuccess) {
       const hipError_t e = launch_range_bounds(a, P, bounds, (int)st->num_cus * 8, stream);
       if (e != hipSuccess) {

@@ -445,17 +445,17 @@ __device__ __forceinline__ void byte_ranges(const RaggedArgs& a, uint64_t wave, 
 }
 
 // The chunked sweep's ranges: bounds[i] = f(i) for i in [0, P] (byte_ranges
-// with P pieces), one wave per two of them.
+// with P pieces; 32-bit, the sweep is for n < 2^32 - 1), one wave per two.
 template <uint32_t kExt>
-__global__ __launch_bounds__(256) void range_bounds_kernel(RaggedArgs args, uint64_t P, uint64_t* bounds) {
+__global__ __launch_bounds__(256) void range_bounds_kernel(RaggedArgs args, uint64_t P, uint32_t* bounds) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t nw = (uint64_t)gridDim.x * 4u;
   for (uint64_t q = (uint64_t)blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
        2 * q <= P; q += nw) {
     uint64_t lo = args.n * (2 * q) / P, hi = 2 * q + 1 <= P ? args.n * (2 * q + 1) / P : args.n;
     byte_ranges<kExt>(args, 2 * q, P, lo, hi);
-    if (lane == 0) bounds[2 * q] = lo;
-    if (lane == 32 && 2 * q + 1 <= P) bounds[2 * q + 1] = hi;
+    if (lane == 0) bounds[2 * q] = (uint32_t)lo;  // (n < 2^32 - 1 here)
+    if (lane == 32 && 2 * q + 1 <= P) bounds[2 * q + 1] = (uint32_t)hi;
   }
 }
 
@@ -503,20 +503,28 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   // indices relative to the wave's first block.)  Other batches: one range
   // per wave, equal counts, or equal bytes for general batches (whose lengths
   // may be skewed; SSTable blocks and log records are near-uniform).
-  const uint64_t* __restrict__ bnd = args.bounds;
-  const bool chunked = bnd != nullptr;
-  const uint64_t nchunks = args.nchunks;
+  constexpr bool kChunkable = (kMode == kModeOut || kMode == kModeVerify) &&
+                              (kExt == kExtOffsets || kExt == kExtHandles);
+  const uint32_t* __restrict__ bnd = args.bounds;
+  const bool chunked = kChunkable && bnd != nullptr;
+  // piece index c * nwaves + w of the range being walked, and the end of the
+  // pieces (nchunks * nwaves < 2^32); 32-bit, to spare scalar registers
+  uint32_t pi = (uint32_t)wave;
+  const uint32_t p_end = (uint32_t)(args.nchunks * nwaves);
   uint64_t b_lo = args.n * wave / nwaves, b_hi = args.n * (wave + 1) / nwaves;
-  uint64_t ck = 0;                      // the chunk being walked
-  uint64_t pf_lo = 0, pf_hi = 0;        // chunk ck + 1's range, loaded a chunk ahead
-  auto chunk_bounds = [&](uint64_t c, uint64_t& lo, uint64_t& hi) {  // c < nchunks
-    lo = bnd[c * nwaves + wave];
-    hi = bnd[c * nwaves + wave + 1];
+#ifndef LSBM_NO_BOUNDS_PREFETCH  // A/B builds only
+  uint32_t pf_lo = 0, pf_hi = 0;  // the next chunk's range, loaded a chunk ahead
+#endif
+  auto piece = [&](uint32_t i, auto& lo, auto& hi) {  // i < p_end
+    lo = bnd[i];
+    hi = bnd[i + 1];
   };
   if (chunked) {
-    chunk_bounds(0, b_lo, b_hi);
-    while (b_lo >= b_hi && ck + 1 < nchunks) chunk_bounds(++ck, b_lo, b_hi);  // (empty ranges)
-    if (ck + 1 < nchunks) chunk_bounds(ck + 1, pf_lo, pf_hi);
+    piece(pi, b_lo, b_hi);
+    while (b_lo >= b_hi && pi + nwaves < p_end) piece(pi += (uint32_t)nwaves, b_lo, b_hi);  // (empty)
+#ifndef LSBM_NO_BOUNDS_PREFETCH
+    if (pi + nwaves < p_end) piece(pi + (uint32_t)nwaves, pf_lo, pf_hi);
+#endif
   } else {
 #ifndef LSBM_NO_BALANCE  // A/B builds only
     // (log records too by bytes, keyed on header offsets: 3 points slower on a
@@ -741,12 +749,18 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     uint32_t no = cur_o + 8 - pre8;
     uint64_t next_hi = range_hi;
     if (chunked && nb >= range_hi) {  // (wave-uniform) this range is done: the next chunk's
-      if (ck + 1 < nchunks) {
-        ck++;
+      if (pi + nwaves < p_end) {
+        pi += (uint32_t)nwaves;
+#ifndef LSBM_NO_BOUNDS_PREFETCH
         nb = pf_lo;
         next_hi = pf_hi;
-        while (nb >= next_hi && ck + 1 < nchunks) chunk_bounds(++ck, nb, next_hi);
-        if (ck + 1 < nchunks) chunk_bounds(ck + 1, pf_lo, pf_hi);
+#else
+        piece(pi, nb, next_hi);
+#endif
+        while (nb >= next_hi && pi + nwaves < p_end) piece(pi += (uint32_t)nwaves, nb, next_hi);
+#ifndef LSBM_NO_BOUNDS_PREFETCH
+        if (pi + nwaves < p_end) piece(pi + (uint32_t)nwaves, pf_lo, pf_hi);
+#endif
       } else {
         nb = next_hi = range_hi;  // (the last chunk: done)
       }
@@ -829,13 +843,44 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
     rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 16));
     rows_max = max(rows_max, (uint32_t)__shfl_xor((int)rows_max, 32));
     rows_max = __builtin_amdgcn_readfirstlane(rows_max);
+    // ... and, in the SSTable modes, the shortest (0 with an idle group):
+    // rows 1 .. rows_min - 2 of every unit are whole rows of its block, loaded
+    // without the select below.  (A/B, profiles/r02/ab/s66_row_fast.log: SST
+    // verify / trailer CRCs +1.3-1.5 points, where a round is 8 blocks of 33-34
+    // rows; config 4 -1.5 and WAL records -1.3, where rows_min is mostly small
+    // and the test costs more than it saves.)
+#ifndef LSBM_NO_ROW_FAST  // A/B builds only
+    constexpr bool kRowFast = kMode == kModeSstSeal || kMode == kModeSstVerify || kMode == kModeSstCrc;
+#else
+    constexpr bool kRowFast = false;
+#endif
+    uint32_t rows_min = 0;
+    if constexpr (kRowFast) {
+      rows_min = active ? rows : 0u;
+      rows_min = min(rows_min, (uint32_t)__shfl_xor((int)rows_min, 8));
+      rows_min = min(rows_min, (uint32_t)__shfl_xor((int)rows_min, 16));
+      rows_min = min(rows_min, (uint32_t)__shfl_xor((int)rows_min, 32));
+      rows_min = __builtin_amdgcn_readfirstlane(rows_min);
+    }
 
     // Row r of this lane is loaded from its address when r in [r_lo, r_hi),
     // else from the zero pad.  Branch-free select, and the address pinned in
     // every lane: where a lane's value is dead, hipcc otherwise left that
     // lane's address undefined although the wave still issues the load
     // (observed: reads below the batch, a GPU fault).
+    //
+    // Rows 1 .. rows_min - 2 (SSTable modes; a wave-uniform test) need no
+    // select: only a unit's row 0 can hold chunks before s (r_lo <= 1) and only
+    // its last row chunks at or past e (r_hi >= rows - 1), so there every
+    // lane's chunk is in [s, e) and the address is the row's own.
     auto row_addr = [&](uint32_t r) -> gptr_u32x4 {
+      if constexpr (kRowFast) {
+        if (r >= 1u && r + 1u < rows_min) {
+          uint64_t p = row_a + (uint64_t)r * kRowBytes;
+          asm volatile("" : "+v"(p));
+          return reinterpret_cast<gptr_u32x4>(p);
+        }
+      }
       const bool ok = (r >= r_lo) & (r < r_hi);
       uint64_t p = ok ? row_a + (uint64_t)r * kRowBytes : dummy;
       asm volatile("" : "+v"(p));
@@ -1138,7 +1183,7 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
   return hipGetLastError();
 }
 
-hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint64_t* bounds, int grid,
+hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint32_t* bounds, int grid,
                                hipStream_t stream) {
   const uint64_t want = (P / 2 + 1 + 3) / 4;  // 4 waves per workgroup, two bounds per wave
   const dim3 g((unsigned)(want < (uint64_t)grid ? want : grid));

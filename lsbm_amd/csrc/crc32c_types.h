@@ -106,7 +106,7 @@ struct RaggedArgs {
   // Chunked sweep (general Out / Verify batches of >= 8 chunks): wave w's
   // range in chunk c is [bounds[c * nwaves + w], bounds[c * nwaves + w + 1]),
   // c < nchunks, from range_bounds_kernel; null: one range per wave.
-  const uint64_t* bounds;
+  const uint32_t* bounds;
   uint64_t nchunks;
 };
 

@@ -143,6 +143,28 @@ def c4uniform(args):
     del d, do
 
 
+def c4sorted(args):
+    """(diagnostic) config 4's exact block lengths, sorted (descending): the
+    same bytes with every round's 8 units alike -- the lock-step loss."""
+    import torch
+    from lsbm_amd import engine
+    n = args.c4_blocks
+    lens = np.sort(zipf_lengths(n))[::-1].copy()
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    offs += 5
+    d = torch.empty(int(offs[-1]) + 16, dtype=torch.uint8, device="cuda")
+    engine.fill_splitmix64(d, 0x5EED0003)
+    do = torch.from_numpy(offs).to("cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    t = time_launches(lambda: engine.crc32c_batch(d, do, out=out, stream=s), s, reps=5, warm=1)
+    gbps = int(lens.sum()) / t / 1e9
+    print(json.dumps({"config": "c4sorted", "blocks": n, "ms": round(t * 1e3, 3),
+                      "pct_hbm_peak": round(100 * gbps / HBM, 2)}), flush=True)
+    del d, do
+
+
 def usweep(args):
     """(diagnostic) equal-length blocks through the ragged kernel, 16 GiB per
     length, 5 bytes off alignment: the per-round cost against the unit count."""
@@ -419,7 +441,7 @@ def main():
     from lsbm_amd import engine
     engine.init(0)
     for w in args.which:
-        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "usweep": usweep, "config1": config1, "config3": config3, "config4": config4, "host": host_staged,
+        {"sst4118": sst4118, "units4k": units4k, "c4uniform": c4uniform, "c4sorted": c4sorted, "usweep": usweep, "config1": config1, "config3": config3, "config4": config4, "host": host_staged,
          "wal": wal}[w](args)
 
 
