@@ -168,6 +168,16 @@ __device__ __forceinline__ uint32_t load32(const uint8_t* p, uint32_t i) {
   }
 }
 
+// lane % d for lane < 64 and 1 <= d < 64 (an overlapping copy's source
+// index): float reciprocal and one correction each way, not the integer
+// division sequence.
+__device__ __forceinline__ uint32_t lane_mod(uint32_t lane, uint32_t d) {
+  const uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)d));
+  int32_t r = (int32_t)lane - (int32_t)(q * d);
+  r = r < 0 ? r + (int32_t)d : (r >= (int32_t)d ? r - (int32_t)d : r);
+  return (uint32_t)r;
+}
+
 // snappy::GetUncompressedLength (varint32, <= 5 bytes, 5th < 16).
 // Returns the preamble size, 0 on failure.
 __device__ __forceinline__ uint32_t parse_preamble(const uint8_t* p, uint64_t n, uint32_t* ulen) {
@@ -245,7 +255,7 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
       // byte j of the copy is out[op - off + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it.
       if (lane < len) {
-        const uint32_t k = off >= len ? lane : lane % off;
+        const uint32_t k = off >= len ? lane : lane_mod(lane, off);
         out[op + lane] = out[op - off + k];
       }
       ip = nip;
@@ -321,7 +331,7 @@ __device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, ui
         // byte j of the copy is out[op - off + j mod off]: an overlapping copy
         // (off < len) repeats its first off bytes, all written before it.
         if (lane < tlen) {
-          const uint32_t k = toff >= tlen ? lane : lane % toff;
+          const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
           out[op + lane] = out[op - toff + k];
         }
         ip += th;
@@ -333,6 +343,150 @@ __device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, ui
       // reordering them
       wave_order();
     }
+  }
+  return op == ulen;
+}
+
+// decode<true> with everything but the copies done lane-parallel, 64 input
+// bytes per step.  The windows are fixed: [ip, ip + 64), ip = 0, 64, 128, ...
+// (a tag or a literal's data may straddle two of them).
+//  1. Every lane parses the tag that WOULD start at its byte (as in
+//     decode_windowed).
+//  2. A scalar walk over the real tags of the window (readlane of each tag's
+//     size) marks them in a 64-bit mask and hands each its output offset
+//     (a lane select): two scalar adds per tag.
+//  3. Every real tag is checked at once against the conditions RawUncompress
+//     tests (header or literal past the stream, offset 0 or before the output,
+//     output past ulen).  The decode fails iff one of them fails: the tags up
+//     to the first failing one are exactly the ones the serial walk visits,
+//     and past it the result is "fail" whatever the rest holds.  Nothing is
+//     written for a window with a failing tag, so a corrupt stream never
+//     writes outside the output window.
+//  4. Literal bytes: lane l owns input byte ip + l (the low byte of its parse
+//     word); it belongs to the data of the last real tag at or before l, or,
+//     below the window's first tag, to a literal that began in an earlier
+//     window.  One byte store per lane, for every literal of the window.
+//  5. Copies, in stream order, each spread over the lanes (one LDS round trip
+//     each).  A copy reads only output before its own, written by earlier
+//     copies or by literals (step 4, issued before).
+// Same accept / reject decisions as decode() (tests/test_snappy.py).
+__device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
+  constexpr uint32_t kLenCap = 0x4000u;  // > any valid length here (ulen < the 16 KiB slice)
+  uint32_t op = 0;    // output offset of the next tag
+  uint32_t next = 0;  // input position of the next tag
+  // a literal's data [lit_lo, lit_hi) that runs into later windows; out[lit_out] <- in[lit_lo]
+  uint32_t lit_lo = 0, lit_hi = 0, lit_out = 0;
+  for (uint32_t ip = 0; ip < cl; ip += 64) {
+    const uint64_t w = load8<true>(in, ip + lane, cl);
+    const uint32_t c = (uint32_t)w & 0xffu;
+    const uint32_t kind = c & 3u;
+    uint32_t hdr, len, off = 0;
+    if (kind == 0) {
+      const uint32_t len0 = (c >> 2) + 1;
+      const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;
+      const uint64_t m = nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1);
+      const uint64_t lx = ((w >> 8) & m) + 1;
+      len = nb ? (lx > 0xffffffffull ? 0xffffffffu : (uint32_t)lx) : len0;
+      hdr = 1 + nb;
+    } else if (kind == 1) {
+      hdr = 2;
+      len = 4 + ((c >> 2) & 7u);
+      off = ((c >> 5) << 8) | (uint32_t)((w >> 8) & 0xffu);
+    } else if (kind == 2) {
+      hdr = 3;
+      len = (c >> 2) + 1;
+      off = (uint32_t)((w >> 8) & 0xffffu);
+    } else {
+      hdr = 5;
+      len = (c >> 2) + 1;
+      off = (uint32_t)((w >> 8) & 0xffffffffu);
+    }
+    const uint32_t lenc = len < kLenCap ? len : kLenCap;
+    const uint32_t size = hdr + (kind == 0 ? lenc : 0u);
+    // 2. the real tags of this window and their output offsets (from op)
+    uint64_t real = 0;
+    uint32_t opt = 0, opa = 0;
+    uint32_t s = next - ip;
+    const uint32_t lim = cl - ip;
+    while (s < 64u && s < lim) {
+      real |= 1ull << s;
+      opt = lane == s ? opa : opt;
+      opa += (uint32_t)__builtin_amdgcn_readlane((int)lenc, (int)s);
+      s += (uint32_t)__builtin_amdgcn_readlane((int)size, (int)s);
+    }
+    const bool me = (real >> lane) & 1u;
+    if (real) {
+      // 3. every real tag's checks (a literal's extra length bytes past the
+      // stream are hdr > rem, like a copy's offset bytes)
+      const uint32_t rem = cl - (ip + lane);
+      const uint32_t o = op + opt;
+      const bool bad = kind == 0 ? (hdr > rem || len > rem - hdr || len > ulen - o)
+                                 : (hdr > rem || off == 0 || off > o || len > ulen - o);
+      if (__ballot(me && bad)) return false;
+    }
+    // 4. literal bytes: the tag owning this lane's byte (the last real tag at
+    // or before it) and its data range, or the literal carried in
+    const uint32_t pack = kind | (hdr << 2) | ((len < 127u ? len : 127u) << 5) | (opt << 12);
+    const uint64_t below = real & (~0ull >> (63u - lane));
+    const uint32_t own = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+    const uint32_t po = (uint32_t)__shfl((int)pack, (int)own);
+    uint32_t dlo = lit_lo, dhi = lit_hi, dout = lit_out;
+    if (below) {
+      const uint32_t d0 = ip + own + ((po >> 2) & 7u);
+      dlo = d0;
+      dhi = (po & 3u) == 0 ? d0 + ((po >> 5) & 127u) : d0;  // (a copy owns no data)
+      dout = op + (po >> 12);
+    }
+    const uint32_t pos = ip + lane;
+    if (pos >= dlo && pos < dhi) out[dout + (pos - dlo)] = (uint8_t)c;
+    if (real) {  // the last tag's literal data may run into the next windows
+      const uint32_t t = 63u - (uint32_t)__builtin_clzll(real);
+      const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)kind, (int)t);
+      const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)hdr, (int)t);
+      const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)lenc, (int)t);
+      lit_lo = ip + t + th;
+      lit_hi = tk == 0 ? lit_lo + tl : lit_lo;
+      lit_out = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t);
+    }
+    // 5. the copies, in order
+    uint64_t cm = real & __ballot(kind != 0);
+    while (cm) {
+      wave_order();
+      const uint32_t t = (uint32_t)__builtin_ctzll(cm);
+      cm &= cm - 1;
+      const uint32_t toff = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)t);
+      const uint32_t tlen = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)t);
+      const uint32_t to = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t);
+#ifdef LSBM_SNAP_COPY_PAIRS  // A/B builds only (6% slower: profiles/r02/snappy/ab_lanes.log)
+      // Two copies per LDS round trip when the second reads nothing the
+      // first writes: its source ends at or before the first's output.  (An
+      // overlapping copy, off < len, reads up to its own output: never paired.)
+      if (cm) {
+        const uint32_t t2 = (uint32_t)__builtin_ctzll(cm);
+        const uint32_t toff2 = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)t2);
+        const uint32_t tlen2 = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)t2);
+        const uint32_t to2 = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t2);
+        if (toff2 >= tlen2 && to2 - toff2 + tlen2 <= to) {
+          cm &= cm - 1;
+          const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
+          const uint8_t v1 = lane < tlen ? out[to - toff + k] : (uint8_t)0;
+          const uint8_t v2 = lane < tlen2 ? out[to2 - toff2 + lane] : (uint8_t)0;
+          if (lane < tlen) out[to + lane] = v1;
+          if (lane < tlen2) out[to2 + lane] = v2;
+          continue;
+        }
+      }
+#endif
+      // byte j of the copy is out[to - off + j mod off]: an overlapping copy
+      // (off < len) repeats its first off bytes, all written before it
+      if (lane < tlen) {
+        const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
+        out[to + lane] = out[to - toff + k];
+      }
+    }
+    wave_order();
+    op += opa;
+    next = ip + s;
   }
   return op == ulen;
 }
@@ -364,10 +518,12 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     uint8_t* win = smem + cl_pad;
     wave_phase();
     SNAP_STAMP(1);
-#ifdef LSBM_SNAP_SERIAL_DECODE  // A/B builds only
+#if defined(LSBM_SNAP_SERIAL_DECODE)  // A/B builds only
     ok = decode<true>(lds_in, cl, win, ulen, lane);
-#else
+#elif defined(LSBM_SNAP_WINDOWED_DECODE)  // A/B builds only: round 2's per-tag walk
     ok = decode_windowed(lds_in, cl, win, ulen, lane);
+#else
+    ok = decode_lanes(lds_in, cl, win, ulen, lane);
 #endif
     SNAP_STAMP(2);
 #ifndef LSBM_SNAP_DIAG_NO_OUT  // diagnostic build only (tools/snappy_diag.py): skips the output, wrong results

@@ -1,0 +1,156 @@
+"""Python model of the snappy decoder's lane-parallel window walk
+(decode_lanes in lsbm_amd/csrc/snappy_kernels.hip), checked on the CPU
+against the snappy oracle (oracle/snappy_oracle.c so_uncompress) on
+compressed blocks of every fixture shape and their corruptions.  A design
+check for the kernel's accept / reject logic, run in the build container:
+
+    python tools/snappy_lanes_model.py
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+
+M32 = 0xffffffff
+
+
+def parse_tag(buf, p):
+    """kind, hdr, len, off of the tag that would start at byte p (bytes past
+    the buffer read as zero), as every lane parses it."""
+    w = 0
+    for k in range(8):
+        w |= (buf[p + k] if p + k < len(buf) else 0) << (8 * k)
+    c = w & 0xff
+    kind = c & 3
+    off = 0
+    if kind == 0:
+        len0 = (c >> 2) + 1
+        nb = len0 - 60 if len0 > 60 else 0
+        m = 0xffffffff if nb == 4 else (1 << (8 * nb)) - 1
+        lx = ((w >> 8) & m) + 1
+        ln = (min(lx, 0xffffffff) if nb else len0)
+        hdr = 1 + nb
+    elif kind == 1:
+        hdr, ln, off = 2, 4 + ((c >> 2) & 7), ((c >> 5) << 8) | ((w >> 8) & 0xff)
+    elif kind == 2:
+        hdr, ln, off = 3, (c >> 2) + 1, (w >> 8) & 0xffff
+    else:
+        hdr, ln, off = 5, (c >> 2) + 1, (w >> 8) & 0xffffffff
+    return c, kind, hdr, ln, off
+
+
+def decode_lanes(inp, ulen):
+    """(ok, out) exactly as the kernel computes them (32-bit unsigned arithmetic)."""
+    cl = len(inp)
+    out = bytearray(ulen)
+    cap = 0x4000
+    op = nxt = 0
+    lit_lo = lit_hi = lit_out = 0
+    ip = 0
+    while ip < cl:
+        lanes = [parse_tag(inp, ip + l) for l in range(64)]
+        lenc = [min(t[3], cap) for t in lanes]
+        size = [t[2] + (lenc[l] if t[1] == 0 else 0) for l, t in enumerate(lanes)]
+        real, opt, opa = [], [0] * 64, 0
+        s, lim = nxt - ip, cl - ip
+        while s < 64 and s < lim:
+            real.append(s)
+            opt[s] = opa
+            opa += lenc[s]
+            s += size[s]
+        for t in real:  # the checks, every real tag at once
+            c, kind, hdr, ln, off = lanes[t]
+            rem = (cl - (ip + t)) & M32
+            o = (op + opt[t]) & M32
+            if kind == 0:
+                bad = hdr > rem or ln > ((rem - hdr) & M32) or ln > ((ulen - o) & M32)
+            else:
+                bad = hdr > rem or off == 0 or off > o or ln > ((ulen - o) & M32)
+            if bad:
+                return False, b""
+        for l in range(64):  # literal bytes
+            below = [t for t in real if t <= l]
+            if below:
+                own = below[-1]
+                _, kind, hdr, ln, _ = lanes[own]
+                dlo = ip + own + hdr
+                dhi = dlo + min(ln, 127) if kind == 0 else dlo
+                dout = op + opt[own]
+            else:
+                dlo, dhi, dout = lit_lo, lit_hi, lit_out
+            pos = ip + l
+            if dlo <= pos < dhi:
+                out[dout + pos - dlo] = lanes[l][0]
+        if real:
+            t = real[-1]
+            _, kind, hdr, _, _ = lanes[t]
+            lit_lo = ip + t + hdr
+            lit_hi = lit_lo + lenc[t] if kind == 0 else lit_lo
+            lit_out = op + opt[t]
+        copies = [t for t in real if lanes[t][1] != 0]
+        i = 0
+        while i < len(copies):  # in order; pairs as the kernel forms them
+            t = copies[i]
+            _, _, _, tlen, toff = lanes[t]
+            to = op + opt[t]
+            if i + 1 < len(copies):
+                t2 = copies[i + 1]
+                _, _, _, tlen2, toff2 = lanes[t2]
+                to2 = op + opt[t2]
+                if toff2 >= tlen2 and to2 - toff2 + tlen2 <= to:
+                    v1 = [out[to - toff + (l if toff >= tlen else l % toff)] for l in range(tlen)]
+                    v2 = [out[to2 - toff2 + l] for l in range(tlen2)]
+                    out[to:to + tlen] = bytes(v1)
+                    out[to2:to2 + tlen2] = bytes(v2)
+                    i += 2
+                    continue
+            v = [out[to - toff + (l if toff >= tlen else l % toff)] for l in range(tlen)]
+            out[to:to + tlen] = bytes(v)
+            i += 1
+        op += opa
+        nxt = ip + s
+        ip += 64
+    return op == ulen, bytes(out) if op == ulen else b""
+
+
+def main():
+    import json
+    from conftest import SnappyOracle
+    from snappy_inputs import block, mutations, varint32
+    from test_snappy import crafted_bytes
+    oracle = SnappyOracle(os.path.join(REPO, "oracle", "liboracle_snappy.so"))
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", "snappy_fixture.json")))
+    n = bad = 0
+
+    def check(stream, what):
+        nonlocal n, bad
+        okp, ulen = oracle.uncompressed_length(stream)
+        want = oracle.uncompress(stream)
+        if not okp or ulen > 0x3000:  # the kernel's LDS path only (ulen < the slice)
+            return
+        i = 0
+        while stream[i] >= 128:
+            i += 1
+        got = decode_lanes(stream[i + 1:], ulen)
+        n += 1
+        if got != want:
+            bad += 1
+            print("MISMATCH", what, got[0], want[0])
+
+    for k, cs in enumerate(gold["cases"]):
+        c = oracle.compress(block(cs["kind"], cs["n"], cs["seed"]))
+        check(c, (cs["kind"], cs["n"]))
+        for name, m in mutations(c, 7000 + k):
+            check(m, (cs["kind"], cs["n"], name))
+    for rec in gold["crafted"]:
+        if rec["name"] != "literal_ext3":
+            check(crafted_bytes(rec["name"], rec), rec["name"])
+    print(f"{n} streams, {bad} mismatches")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
