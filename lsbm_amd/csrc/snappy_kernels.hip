@@ -25,6 +25,8 @@
 namespace lsbm {
 namespace {
 
+typedef const __attribute__((address_space(1))) uint32_t* gcu32;  // global loads, not flat
+
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
@@ -270,91 +272,14 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
   return op == ulen;
 }
 
-// decode<true> with the tag headers parsed 64 input bytes at a time: every
-// lane parses the tag that WOULD start at its byte of the window (kind, header
-// size, length, offset; all lanes at once, from the staged LDS copy), and the
-// wave then walks the real tags through the window reading each one's fields
-// from its lane (readlane: scalar registers) -- the serial part per tag is the
-// validity checks and the byte move, not the header decode.  Same checks in
-// the same order as decode(), so the same streams are rejected.
-__device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
-  uint32_t ip = 0, op = 0;
-  while (ip < cl) {
-    // parse the window [ip, ip + 64): lane l the tag at ip + l (bytes past the
-    // stream are the zero pad or the output slice; only tags whose checks fail
-    // ever use them)
-    const uint64_t w = load8<true>(in, ip + lane, cl);
-    const uint32_t c = (uint32_t)w & 0xffu;
-    const uint32_t kind = c & 3u;
-    uint32_t hdr, len, off = 0;
-    if (kind == 0) {
-      const uint32_t len0 = (c >> 2) + 1;
-      const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;
-      const uint64_t m = nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1);
-      const uint64_t lx = ((w >> 8) & m) + 1;  // (nb = 0: m = 0, lx = 1)
-      len = nb ? (lx > 0xffffffffull ? 0xffffffffu : (uint32_t)lx) : len0;  // (saturated: fails anyway)
-      hdr = 1 + nb;
-    } else if (kind == 1) {
-      hdr = 2;
-      len = 4 + ((c >> 2) & 7u);
-      off = ((c >> 5) << 8) | (uint32_t)((w >> 8) & 0xffu);
-    } else if (kind == 2) {
-      hdr = 3;
-      len = (c >> 2) + 1;
-      off = (uint32_t)((w >> 8) & 0xffffu);
-    } else {
-      hdr = 5;
-      len = (c >> 2) + 1;
-      off = (uint32_t)((w >> 8) & 0xffffffffu);
-    }
-    const uint32_t meta = kind | (hdr << 2);
-    // walk the tags that start inside this window
-    uint32_t s = 0;
-    // (one path for both kinds, the checks and byte move selected: 16%
-    // slower, A/B profiles/r02/snappy/ab_walk_single_path.log)
-    while (s < 64u && ip < cl) {
-      const uint32_t mt = __builtin_amdgcn_readlane(meta, s);
-      const uint32_t tlen = __builtin_amdgcn_readlane(len, s);
-      const uint32_t th = mt >> 2;
-      if ((mt & 3u) == 0) {  // literal
-        if (th > 1 && th - 1 > cl - ip - 1) return false;
-        if (tlen > cl - ip - th || tlen > ulen - op) return false;
-        const uint8_t* src = in + ip + th;
-        uint8_t* dst = out + op;
-        for (uint32_t j = lane; j < tlen; j += 64) dst[j] = src[j];
-        ip += th + tlen;
-        op += tlen;
-        s += th + tlen;  // (a long literal ends the window)
-      } else {  // copy
-        const uint32_t toff = __builtin_amdgcn_readlane(off, s);
-        if (th > cl - ip || toff == 0 || toff > op || tlen > ulen - op) return false;
-        // byte j of the copy is out[op - off + j mod off]: an overlapping copy
-        // (off < len) repeats its first off bytes, all written before it.
-        if (lane < tlen) {
-          const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
-          out[op + lane] = out[op - toff + k];
-        }
-        ip += th;
-        op += tlen;
-        s += th;
-      }
-      // one wave's LDS accesses execute in issue order: a copy reads the bytes
-      // earlier tags wrote without waiting; this only keeps the compiler from
-      // reordering them
-      wave_order();
-    }
-  }
-  return op == ulen;
-}
-
-// decode<true> with everything but the copies done lane-parallel, 64 input
-// bytes per step.  The windows are fixed: [ip, ip + 64), ip = 0, 64, 128, ...
-// (a tag or a literal's data may straddle two of them).
-//  1. Every lane parses the tag that WOULD start at its byte (as in
-//     decode_windowed).
-//  2. A scalar walk over the real tags of the window (readlane of each tag's
-//     size) marks them in a 64-bit mask and hands each its output offset
-//     (a lane select): two scalar adds per tag.
+// The tag walk lane-parallel, 64 input bytes per step.  The windows are
+// fixed: [ip, ip + 64), ip = 0, 64, 128, ... (a tag or a literal's data may
+// straddle two of them).
+//  1. Every lane parses the tag that WOULD start at its byte (branch-free:
+//     kind, header size, length, offset).
+//  2. A scalar walk over the real tags of the window (one readlane of each
+//     tag's size and length) marks them in a 64-bit mask and hands each its
+//     output offset (a lane select): two scalar adds per tag.
 //  3. Every real tag is checked at once against the conditions RawUncompress
 //     tests (header or literal past the stream, offset 0 or before the output,
 //     output past ulen).  The decode fails iff one of them fails: the tags up
@@ -368,41 +293,56 @@ __device__ bool decode_windowed(const uint8_t* in, uint32_t cl, uint8_t* out, ui
 //     window.  One byte store per lane, for every literal of the window.
 //  5. Copies, in stream order, each spread over the lanes (one LDS round trip
 //     each).  A copy reads only output before its own, written by earlier
-//     copies or by literals (step 4, issued before).
-// Same accept / reject decisions as decode() (tests/test_snappy.py).
+//     copies or by literals (step 4, issued before).  (Pairing two copies per
+//     round trip when the second reads nothing the first writes measured 6%
+//     slower: profiles/r02/snappy/ab_lanes.log.)
+// The compressed bytes are read from global memory (kGlobalIn: two aligned
+// dwords per lane per window, requested one window ahead; no dword past the
+// one holding the last byte), so the wave's LDS slice holds only the output
+// window; or from an LDS copy (A/B builds).  Same accept / reject decisions as
+// decode() (tests/test_snappy.py; tools/snappy_lanes_model.py restates the
+// walk and checks it against the oracle).
+template <bool kGlobalIn>
 __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
   constexpr uint32_t kLenCap = 0x4000u;  // > any valid length here (ulen < the 16 KiB slice)
   uint32_t op = 0;    // output offset of the next tag
   uint32_t next = 0;  // input position of the next tag
   // a literal's data [lit_lo, lit_hi) that runs into later windows; out[lit_out] <- in[lit_lo]
   uint32_t lit_lo = 0, lit_hi = 0, lit_out = 0;
+  const uint64_t gin = reinterpret_cast<uint64_t>(in);
+  const uint64_t last = (gin + (cl ? cl - 1 : 0)) & ~3ull;  // the dword holding in[cl - 1]
+  auto issue = [&](uint32_t i, uint32_t& lo, uint32_t& hi) {  // (global input only)
+    const uint64_t a0 = (gin + i) & ~3ull;
+    lo = *reinterpret_cast<gcu32>(a0 < last ? a0 : last);
+    hi = *reinterpret_cast<gcu32>(a0 + 4 < last ? a0 + 4 : last);
+  };
+  uint32_t lo = 0, hi = 0;
+  if (kGlobalIn && cl) issue(lane, lo, hi);
+  const uint64_t upto = ~0ull >> (63u - lane);  // lanes 0 .. lane
   for (uint32_t ip = 0; ip < cl; ip += 64) {
-    const uint64_t w = load8<true>(in, ip + lane, cl);
-    const uint32_t c = (uint32_t)w & 0xffu;
-    const uint32_t kind = c & 3u;
-    uint32_t hdr, len, off = 0;
-    if (kind == 0) {
-      const uint32_t len0 = (c >> 2) + 1;
-      const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;
-      const uint64_t m = nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1);
-      const uint64_t lx = ((w >> 8) & m) + 1;
-      len = nb ? (lx > 0xffffffffull ? 0xffffffffu : (uint32_t)lx) : len0;
-      hdr = 1 + nb;
-    } else if (kind == 1) {
-      hdr = 2;
-      len = 4 + ((c >> 2) & 7u);
-      off = ((c >> 5) << 8) | (uint32_t)((w >> 8) & 0xffu);
-    } else if (kind == 2) {
-      hdr = 3;
-      len = (c >> 2) + 1;
-      off = (uint32_t)((w >> 8) & 0xffffu);
+    uint64_t w;
+    if constexpr (kGlobalIn) {
+      uint32_t nlo, nhi;
+      issue(ip + 64 + lane, nlo, nhi);  // the next window's words
+      w = (((uint64_t)hi << 32) | lo) >> (8 * ((uint32_t)(gin + ip + lane) & 3u));
+      lo = nlo;
+      hi = nhi;
     } else {
-      hdr = 5;
-      len = (c >> 2) + 1;
-      off = (uint32_t)((w >> 8) & 0xffffffffu);
+      w = load8<true>(in, ip + lane, cl);
     }
+    // 1. the tag at this lane's byte
+    const uint32_t c = (uint32_t)w & 0xffu;
+    const uint32_t x = (uint32_t)(w >> 8);  // the 4 bytes after the tag byte
+    const uint32_t kind = c & 3u;
+    const uint32_t len0 = (c >> 2) + 1;
+    const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;  // a literal's extra length bytes
+    const uint32_t xm = nb == 4 ? x : x & ((1u << (8 * nb)) - 1u);
+    const uint32_t len_lit = nb ? (xm == 0xffffffffu ? xm : xm + 1) : len0;  // (saturated: fails anyway)
+    const uint32_t hdr = kind == 0 ? 1 + nb : (kind == 1 ? 2u : (kind == 2 ? 3u : 5u));
+    const uint32_t len = kind == 0 ? len_lit : (kind == 1 ? 4 + ((c >> 2) & 7u) : len0);
+    const uint32_t off = kind == 1 ? ((c >> 5) << 8) | (x & 0xffu) : (kind == 2 ? x & 0xffffu : x);
     const uint32_t lenc = len < kLenCap ? len : kLenCap;
-    const uint32_t size = hdr + (kind == 0 ? lenc : 0u);
+    const uint32_t ws = (hdr + (kind == 0 ? lenc : 0u)) | (lenc << 16);  // size | output length
     // 2. the real tags of this window and their output offsets (from op)
     uint64_t real = 0;
     uint32_t opt = 0, opa = 0;
@@ -411,23 +351,24 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     while (s < 64u && s < lim) {
       real |= 1ull << s;
       opt = lane == s ? opa : opt;
-      opa += (uint32_t)__builtin_amdgcn_readlane((int)lenc, (int)s);
-      s += (uint32_t)__builtin_amdgcn_readlane((int)size, (int)s);
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ws, (int)s);
+      opa += v >> 16;
+      s += v & 0xffffu;
     }
-    const bool me = (real >> lane) & 1u;
+    const uint32_t o = op + opt;
     if (real) {
       // 3. every real tag's checks (a literal's extra length bytes past the
       // stream are hdr > rem, like a copy's offset bytes)
+      const bool me = (real >> lane) & 1u;
       const uint32_t rem = cl - (ip + lane);
-      const uint32_t o = op + opt;
-      const bool bad = kind == 0 ? (hdr > rem || len > rem - hdr || len > ulen - o)
-                                 : (hdr > rem || off == 0 || off > o || len > ulen - o);
+      const bool bad = hdr > rem || len > ulen - o ||
+                       (kind == 0 ? len > rem - hdr : (off == 0 || off > o));
       if (__ballot(me && bad)) return false;
     }
     // 4. literal bytes: the tag owning this lane's byte (the last real tag at
     // or before it) and its data range, or the literal carried in
     const uint32_t pack = kind | (hdr << 2) | ((len < 127u ? len : 127u) << 5) | (opt << 12);
-    const uint64_t below = real & (~0ull >> (63u - lane));
+    const uint64_t below = real & upto;
     const uint32_t own = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
     const uint32_t po = (uint32_t)__shfl((int)pack, (int)own);
     uint32_t dlo = lit_lo, dhi = lit_hi, dout = lit_out;
@@ -441,47 +382,28 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     if (pos >= dlo && pos < dhi) out[dout + (pos - dlo)] = (uint8_t)c;
     if (real) {  // the last tag's literal data may run into the next windows
       const uint32_t t = 63u - (uint32_t)__builtin_clzll(real);
-      const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)kind, (int)t);
-      const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)hdr, (int)t);
-      const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)lenc, (int)t);
-      lit_lo = ip + t + th;
-      lit_hi = tk == 0 ? lit_lo + tl : lit_lo;
-      lit_out = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t);
+      const uint32_t tp = (uint32_t)__builtin_amdgcn_readlane((int)pack, (int)t);
+      const uint32_t tw = (uint32_t)__builtin_amdgcn_readlane((int)ws, (int)t);
+      lit_lo = ip + t + ((tp >> 2) & 7u);
+      lit_hi = (tp & 3u) == 0 ? lit_lo + (tw >> 16) : lit_lo;
+      lit_out = op + (tp >> 12);
     }
-    // 5. the copies, in order
+    // 5. the copies, in order: output [dst, dst + len) from [dst - off, ...)
+    const uint32_t cpa = o | ((len - 1) << 16);  // (a valid copy: o < 2^14, len <= 64)
+    const uint32_t cps = o - off;
     uint64_t cm = real & __ballot(kind != 0);
     while (cm) {
       wave_order();
       const uint32_t t = (uint32_t)__builtin_ctzll(cm);
       cm &= cm - 1;
-      const uint32_t toff = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)t);
-      const uint32_t tlen = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)t);
-      const uint32_t to = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t);
-#ifdef LSBM_SNAP_COPY_PAIRS  // A/B builds only (6% slower: profiles/r02/snappy/ab_lanes.log)
-      // Two copies per LDS round trip when the second reads nothing the
-      // first writes: its source ends at or before the first's output.  (An
-      // overlapping copy, off < len, reads up to its own output: never paired.)
-      if (cm) {
-        const uint32_t t2 = (uint32_t)__builtin_ctzll(cm);
-        const uint32_t toff2 = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)t2);
-        const uint32_t tlen2 = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)t2);
-        const uint32_t to2 = op + (uint32_t)__builtin_amdgcn_readlane((int)opt, (int)t2);
-        if (toff2 >= tlen2 && to2 - toff2 + tlen2 <= to) {
-          cm &= cm - 1;
-          const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
-          const uint8_t v1 = lane < tlen ? out[to - toff + k] : (uint8_t)0;
-          const uint8_t v2 = lane < tlen2 ? out[to2 - toff2 + lane] : (uint8_t)0;
-          if (lane < tlen) out[to + lane] = v1;
-          if (lane < tlen2) out[to2 + lane] = v2;
-          continue;
-        }
-      }
-#endif
-      // byte j of the copy is out[to - off + j mod off]: an overlapping copy
+      const uint32_t ta = (uint32_t)__builtin_amdgcn_readlane((int)cpa, (int)t);
+      const uint32_t src = (uint32_t)__builtin_amdgcn_readlane((int)cps, (int)t);
+      const uint32_t dst = ta & 0xffffu, tlen = (ta >> 16) + 1;
+      // byte j of the copy is out[src + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it
       if (lane < tlen) {
-        const uint32_t k = toff >= tlen ? lane : lane_mod(lane, toff);
-        out[to + lane] = out[to - toff + k];
+        const uint32_t k = src + tlen <= dst ? lane : lane_mod(lane, dst - src);
+        out[dst + lane] = out[src + k];
       }
     }
     wave_order();
@@ -491,13 +413,14 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
   return op == ulen;
 }
 
-// Decodes block b with the wave's LDS slice of kSlice bytes when its
-// compressed bytes and output fit, else (kGlobalFallback) against global
-// memory.  Returns 2 when the block neither fits nor may fall back.
+// Decodes block b into the wave's LDS slice of kSlice bytes when its output
+// fits (the compressed bytes are read from global memory; A/B builds with
+// LSBM_SNAP_STAGED_INPUT stage them in the slice too), else
+// (kGlobalFallback) against global memory.  Returns 2 when the block neither
+// fits nor may fall back.
 template <uint32_t kSlice, bool kGlobalFallback>
 __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint64_t b, uint32_t lane
                                                      SNAP_STAMPS_PARAM) {
-  uint8_t* const lds_in = smem;
   const uint64_t s = a.offsets[b], e = a.offsets[b + 1];
   const uint64_t os = a.out_offsets[b], cap = a.out_offsets[b + 1] - os;
   const uint64_t clen = e - s;
@@ -506,24 +429,28 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
   ulen = uni(ulen);
   if (pre == 0 || (uint64_t)ulen > cap) return 0;
   const uint64_t cl64 = clen - pre;
-  const uint32_t cl_pad = (uint32_t)((cl64 + 8 + 15) & ~15ull);
+  if (cl64 >= 0xffffffffull) return 0;  // a >= 4 GiB compressed block (snappy's lengths are 32-bit)
+  const uint8_t* g = a.base + s + pre;
+  const uint32_t cl = (uint32_t)cl64;
   bool ok;
-  if (cl64 + 8 + 15 + (uint64_t)ulen <= kSlice) {
-    const uint8_t* g = a.base + s + pre;
-    const uint32_t cl = (uint32_t)cl64;
+#ifdef LSBM_SNAP_STAGED_INPUT  // A/B builds only: the compressed bytes staged in the slice too
+  const uint64_t need = cl64 + 8 + 15 + (uint64_t)ulen;
+#else
+  const uint64_t need = (uint64_t)ulen + 16;  // (unstage_from_lds reads up to 16 B past ulen)
+#endif
+  if (need <= kSlice) {
     SNAP_STAMP(0);  // offsets + preamble
+#ifdef LSBM_SNAP_STAGED_INPUT
+    uint8_t* const lds_in = smem;
     stage_to_lds(lds_in, g, cl, lane);
     wave_order();
     if (lane < 8) lds_in[cl + lane] = 0;  // zero pad behind the stream (load8 reads <= cl+6)
-    uint8_t* win = smem + cl_pad;
+    uint8_t* win = smem + (uint32_t)((cl64 + 8 + 15) & ~15ull);
     wave_phase();
-    SNAP_STAMP(1);
-#if defined(LSBM_SNAP_SERIAL_DECODE)  // A/B builds only
-    ok = decode<true>(lds_in, cl, win, ulen, lane);
-#elif defined(LSBM_SNAP_WINDOWED_DECODE)  // A/B builds only: round 2's per-tag walk
-    ok = decode_windowed(lds_in, cl, win, ulen, lane);
+    ok = decode_lanes<false>(lds_in, cl, win, ulen, lane);
 #else
-    ok = decode_lanes(lds_in, cl, win, ulen, lane);
+    uint8_t* win = smem;
+    ok = decode_lanes<true>(g, cl, win, ulen, lane);
 #endif
     SNAP_STAMP(2);
 #ifndef LSBM_SNAP_DIAG_NO_OUT  // diagnostic build only (tools/snappy_diag.py): skips the output, wrong results
@@ -533,10 +460,8 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     wave_phase();
   } else if (!kGlobalFallback) {
     return 2;
-  } else if (cl64 < 0xffffffffull) {
-    ok = decode<false>(a.base + s + pre, (uint32_t)cl64, a.out + os, ulen, lane);
   } else {
-    ok = false;  // a >= 4 GiB compressed block (snappy's lengths are 32-bit)
+    ok = decode<false>(g, cl, a.out + os, ulen, lane);
   }
   return ok ? 1 : 0;
 }

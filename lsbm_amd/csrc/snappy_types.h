@@ -11,12 +11,18 @@ namespace lsbm {
 // (the decoder's output; the encoder's fragment bytes, its table staying in
 // LDS).
 constexpr uint32_t kSnapThreads = 64;
-// decoder slices hold the compressed bytes + 8 pad + the output window: pass 1
-// uses small slices (more waves in flight), pass 2 large ones.  7 KiB: a
-// db_bench block (4,117-4,122 B) with its compressed form (~2.3 KB) fits, 22
-// waves per CU (A/B: 8 KiB 171 GB/s, 7 KiB 189 GB/s, 6.5 KiB 187 GB/s).
+// decoder slices hold the output window (the compressed bytes are read from
+// global memory): pass 1 uses small slices (more waves in flight), pass 2
+// large ones.  5 KiB: a db_bench block (4,117-4,122 B) fits, 32 waves per CU
+// (the hardware's maximum).  (Round 2's decoder staged the compressed bytes
+// in the slice too: 7 KiB, 22 waves per CU; A/B 8 / 7 / 6.5 KiB 171 / 189 /
+// 187 GB/s.  A/B builds with LSBM_SNAP_STAGED_INPUT still do.)
 #ifndef LSBM_SNAP_DEC_LDS  // (A/B builds override)
+#ifdef LSBM_SNAP_STAGED_INPUT
 #define LSBM_SNAP_DEC_LDS 7168
+#else
+#define LSBM_SNAP_DEC_LDS 5120
+#endif
 #endif
 constexpr uint32_t kSnapDecLds = LSBM_SNAP_DEC_LDS;
 constexpr uint32_t kSnapDecLdsLarge = 16384;

@@ -91,25 +91,11 @@ def decode_lanes(inp, ulen):
             lit_hi = lit_lo + lenc[t] if kind == 0 else lit_lo
             lit_out = op + opt[t]
         copies = [t for t in real if lanes[t][1] != 0]
-        i = 0
-        while i < len(copies):  # in order; pairs as the kernel forms them
-            t = copies[i]
+        for t in copies:  # in order
             _, _, _, tlen, toff = lanes[t]
             to = op + opt[t]
-            if i + 1 < len(copies):
-                t2 = copies[i + 1]
-                _, _, _, tlen2, toff2 = lanes[t2]
-                to2 = op + opt[t2]
-                if toff2 >= tlen2 and to2 - toff2 + tlen2 <= to:
-                    v1 = [out[to - toff + (l if toff >= tlen else l % toff)] for l in range(tlen)]
-                    v2 = [out[to2 - toff2 + l] for l in range(tlen2)]
-                    out[to:to + tlen] = bytes(v1)
-                    out[to2:to2 + tlen2] = bytes(v2)
-                    i += 2
-                    continue
             v = [out[to - toff + (l if toff >= tlen else l % toff)] for l in range(tlen)]
             out[to:to + tlen] = bytes(v)
-            i += 1
         op += opa
         nxt = ip + s
         ip += 64
