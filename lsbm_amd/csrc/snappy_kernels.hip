@@ -197,6 +197,30 @@ __device__ __forceinline__ uint32_t parse_preamble(const uint8_t* p, uint64_t n,
   return 0;
 }
 
+// parse_preamble over the block's first bytes loaded at once: the two aligned
+// dwords from the one holding p[0] (never a dword past the one holding
+// p[n - 1]), so the varint costs one memory round trip, not one per byte.
+__device__ __forceinline__ uint32_t parse_preamble_wide(const uint8_t* p, uint64_t n, uint32_t* ulen) {
+  if (n == 0) return 0;
+  const uint64_t g = reinterpret_cast<uint64_t>(p);
+  const uint64_t a0 = g & ~3ull, last = (g + n - 1) & ~3ull;
+  const uint32_t lo = *reinterpret_cast<gcu32>(a0);
+  const uint32_t hi = *reinterpret_cast<gcu32>(a0 + 4 <= last ? a0 + 4 : a0);
+  const uint64_t w = (((uint64_t)hi << 32) | lo) >> (8 * (uint32_t)(g & 3u));  // >= 5 valid bytes
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < 5; i++) {
+    if (i >= n) return 0;
+    const uint32_t b = (uint32_t)(w >> (8 * i)) & 0xffu;
+    if (i == 4 && b >= 16) return 0;
+    v |= (b & 127u) << (7 * i);
+    if (b < 128) {
+      *ulen = v;
+      return i + 1;
+    }
+  }
+  return 0;
+}
+
 // ---- decoder ----
 
 // Tag walk of snappy's DecompressAllTags over in[0, cl) into out[0, ulen):
@@ -279,7 +303,7 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 //     kind, header size, length, offset).
 //  2. A scalar walk over the real tags of the window (one readlane of each
 //     tag's size and length) marks them in a 64-bit mask and hands each its
-//     output offset (a lane select): two scalar adds per tag.
+//     output offset (v_writelane): two scalar adds per tag.
 //  3. Every real tag is checked at once against the conditions RawUncompress
 //     tests (header or literal past the stream, offset 0 or before the output,
 //     output past ulen).  The decode fails iff one of them fails: the tags up
@@ -330,17 +354,19 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     } else {
       w = load8<true>(in, ip + lane, cl);
     }
-    // 1. the tag at this lane's byte
+    // 1. the tag at this lane's byte, as selects (no per-kind branches)
     const uint32_t c = (uint32_t)w & 0xffu;
     const uint32_t x = (uint32_t)(w >> 8);  // the 4 bytes after the tag byte
     const uint32_t kind = c & 3u;
     const uint32_t len0 = (c >> 2) + 1;
     const uint32_t nb = len0 > 60 ? len0 - 60 : 0u;  // a literal's extra length bytes
-    const uint32_t xm = nb == 4 ? x : x & ((1u << (8 * nb)) - 1u);
+    // the little-endian field after the tag byte: nb bytes (literal), 1 / 2 / 4 (copies)
+    const uint32_t fb = kind == 0 ? nb : (kind == 3 ? 4u : kind);
+    const uint32_t xm = fb == 4 ? x : x & ((1u << (8 * fb)) - 1u);
     const uint32_t len_lit = nb ? (xm == 0xffffffffu ? xm : xm + 1) : len0;  // (saturated: fails anyway)
-    const uint32_t hdr = kind == 0 ? 1 + nb : (kind == 1 ? 2u : (kind == 2 ? 3u : 5u));
+    const uint32_t hdr = 1 + fb;
     const uint32_t len = kind == 0 ? len_lit : (kind == 1 ? 4 + ((c >> 2) & 7u) : len0);
-    const uint32_t off = kind == 1 ? ((c >> 5) << 8) | (x & 0xffu) : (kind == 2 ? x & 0xffffu : x);
+    const uint32_t off = kind == 1 ? ((c >> 5) << 8) | xm : xm;
     const uint32_t lenc = len < kLenCap ? len : kLenCap;
     const uint32_t ws = (hdr + (kind == 0 ? lenc : 0u)) | (lenc << 16);  // size | output length
     // 2. the real tags of this window and their output offsets (from op)
@@ -350,7 +376,10 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     const uint32_t lim = cl - ip;
     while (s < 64u && s < lim) {
       real |= 1ull << s;
-      opt = lane == s ? opa : opt;
+      // opt[s] = opa: v_writelane (one VALU instead of a compare and a select;
+      // lane select in M0, which no other instruction of these kernels uses --
+      // gfx9's constant bus takes one SGPR besides M0)
+      asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(opt) : "s"(opa), "s"(s) : "m0");
       const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ws, (int)s);
       opa += v >> 16;
       s += v & 0xffffu;
@@ -425,7 +454,7 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
   const uint64_t os = a.out_offsets[b], cap = a.out_offsets[b + 1] - os;
   const uint64_t clen = e - s;
   uint32_t ulen = 0;
-  const uint32_t pre = uni(parse_preamble(a.base + s, clen, &ulen));
+  const uint32_t pre = uni(parse_preamble_wide(a.base + s, clen, &ulen));
   ulen = uni(ulen);
   if (pre == 0 || (uint64_t)ulen > cap) return 0;
   const uint64_t cl64 = clen - pre;
