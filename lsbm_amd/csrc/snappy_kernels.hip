@@ -321,8 +321,8 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 //     round trip when the second reads nothing the first writes measured 6%
 //     slower: profiles/r02/snappy/ab_lanes.log.)
 // The compressed bytes are read from global memory (kGlobalIn: two aligned
-// dwords per lane per window, requested one window ahead; no dword past the
-// one holding the last byte), so the wave's LDS slice holds only the output
+// dwords per lane per window, requested one window ahead, through a buffer
+// descriptor bounded to the dwords holding the stream), so the wave's LDS slice holds only the output
 // window; or from an LDS copy (A/B builds).  Same accept / reject decisions as
 // decode() (tests/test_snappy.py; tools/snappy_lanes_model.py restates the
 // walk and checks it against the oracle).
@@ -333,12 +333,18 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
   uint32_t next = 0;  // input position of the next tag
   // a literal's data [lit_lo, lit_hi) that runs into later windows; out[lit_out] <- in[lit_lo]
   uint32_t lit_lo = 0, lit_hi = 0, lit_out = 0;
+  // global input: a buffer descriptor over the dwords holding in[0, cl), so a
+  // load past them returns zero without touching memory (no address clamps)
   const uint64_t gin = reinterpret_cast<uint64_t>(in);
-  const uint64_t last = (gin + (cl ? cl - 1 : 0)) & ~3ull;  // the dword holding in[cl - 1]
+  const uint32_t sh0 = (uint32_t)gin & 3u;
+  __amdgpu_buffer_rsrc_t rsrc;
+  if constexpr (kGlobalIn)
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(in - sh0), (short)0,
+                                             (int)((sh0 + cl + 3) & ~3u), 0x00020000);
   auto issue = [&](uint32_t i, uint32_t& lo, uint32_t& hi) {  // (global input only)
-    const uint64_t a0 = (gin + i) & ~3ull;
-    lo = *reinterpret_cast<gcu32>(a0 < last ? a0 : last);
-    hi = *reinterpret_cast<gcu32>(a0 + 4 < last ? a0 + 4 : last);
+    const uint32_t a0 = (sh0 + i) & ~3u;
+    lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, a0, 0, 0);
+    hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, a0 + 4, 0, 0);
   };
   uint32_t lo = 0, hi = 0;
   if (kGlobalIn && cl) issue(lane, lo, hi);
@@ -348,7 +354,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     if constexpr (kGlobalIn) {
       uint32_t nlo, nhi;
       issue(ip + 64 + lane, nlo, nhi);  // the next window's words
-      w = (((uint64_t)hi << 32) | lo) >> (8 * ((uint32_t)(gin + ip + lane) & 3u));
+      w = (((uint64_t)hi << 32) | lo) >> (8 * ((sh0 + ip + lane) & 3u));
       lo = nlo;
       hi = nhi;
     } else {
@@ -390,8 +396,10 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
       // stream are hdr > rem, like a copy's offset bytes)
       const bool me = (real >> lane) & 1u;
       const uint32_t rem = cl - (ip + lane);
-      const bool bad = hdr > rem || len > ulen - o ||
-                       (kind == 0 ? len > rem - hdr : (off == 0 || off > o));
+      // (bitwise, not short-circuit: no divergent branches)
+      const bool bad_lit = len > rem - hdr;
+      const bool bad_cp = (off == 0) | (off > o);
+      const bool bad = (hdr > rem) | (len > ulen - o) | ((kind == 0) ? bad_lit : bad_cp);
       if (__ballot(me && bad)) return false;
     }
     // 4. literal bytes: the tag owning this lane's byte (the last real tag at
