@@ -406,6 +406,15 @@ def wal(args):
     ep = ctypes.c_void_p(ext.data_ptr())
     t_ext = time_launches(lambda: L.lsbm_crc32c_extents_dev(dp, ep, n, None, mp, 0, sp), s)
     crc_bytes = int(plen.sum()) + n
+    # (diagnostic) the same headers passed length-sorted within windows of 512
+    # (the kernel takes header offsets in any order): a round's 8 records alike
+    W = 512
+    perm = np.concatenate([i + np.argsort(plen[i:i + W], kind="stable") for i in range(0, n, W)])
+    dhs = torch.from_numpy(heads[perm].astype(heads.dtype)).to("cuda")
+    hsp = ctypes.c_void_p(dhs.data_ptr())
+    t_seal_sorted = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hsp, n, mp, bp, sp), s)
+    nbad.zero_()
+    t_ver_sorted = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hsp, n, op, bp, sp), s)
     o = oracle()
     bad = 0
     for i in range(0, n, max(1, n // 2000)):
@@ -420,6 +429,8 @@ def wal(args):
                       "log_verify": {"ms": round(t_ver * 1e3, 3), "pct_hbm_peak": pct(t_ver),
                                      "all_ok": bool(ok.all().item())},
                       "extents_same_bytes": {"ms": round(t_ext * 1e3, 3), "pct_hbm_peak": pct(t_ext)},
+                      "len_sorted_512": {"seal_pct_hbm_peak": pct(t_seal_sorted), "verify_pct_hbm_peak": pct(t_ver_sorted),
+                                         "verify_all_ok": bool(ok.all().item())},
                       "sample_mismatches": bad}), flush=True)
 
 
