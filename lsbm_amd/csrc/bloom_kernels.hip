@@ -494,10 +494,22 @@ void bloom_build_kernel(BloomBuildArgs a) {
       const uint64_t t = __shfl_up(incl, d);
       if (lane >= d) incl += t;
     }
-    const uint64_t total = readlane64(incl, kBloomGroup - 1);
     const uint64_t kb0 = readlane64(k0, 0), kb1 = readlane64(k1, g - 1);
     const uint64_t next0 = __shfl_down(k0, 1);
     const bool contiguous = lane >= g || (k1 >= k0 && (lane == g - 1 || next0 == k1));
+    // Dense layout: when the group's filters follow each other in the output
+    // (each one's bits, then its k byte: FilterBlockBuilder's result_), LDS
+    // holds the output image itself, at the destination's byte alignment, and
+    // leaves as one run of dword stores (bytes at the two ends).  Otherwise
+    // each filter sits at a dword boundary with a pad word and leaves alone.
+    const uint64_t fo_next = __shfl_down(fo, 1);
+    const bool out_next = lane + 1 >= g || fo_next == fo + bytes + 1;
+    const uint64_t fo0 = readlane64(fo, 0);
+    const uint64_t dst0 = reinterpret_cast<uint64_t>(a.out) + fo0;
+    const uint32_t gsh = (uint32_t)dst0 & 3u;
+    const uint64_t span = readlane64(fo + bytes + 1, g - 1) - fo0;  // (dense: the group's output bytes)
+    const bool dense = __ballot(!out_next) == 0 && span < (1ull << 20);
+    const uint64_t total = dense ? (gsh + span + 3) / 4 : readlane64(incl, kBloomGroup - 1);
     const bool packed = __ballot(!contiguous) == 0 && total <= kBloomRegionWords &&
                         kb1 >= kb0 && kb1 - kb0 < (1ull << 31);
     if (!packed) {
@@ -514,19 +526,23 @@ void bloom_build_kernel(BloomBuildArgs a) {
     uint64_t oa0 = 0, oa1 = 0, ob0 = 0, ob1 = 0;
     if (lane < nkeys) load_off2(ko, lane, oa0, oa1);
     if (lane + 64u < nkeys) load_off2(ko, lane + 64, ob0, ob1);
-    // filter t's constants, from lane t, into slot t: LDS word base, bits d,
+    // filter t's constants, from lane t, into slot t: LDS bit base, bits d,
     // fastmod magic, 2^32 mod d; and (in lane t) its first key relative to the group's (non-decreasing;
     // ~0 past the group, so that a search never selects those lanes)
-    const uint32_t base_t = (uint32_t)(incl - words);
+    const uint32_t base_t = (uint32_t)(incl - words);  // (sparse layout: word base)
+    const uint32_t byte_t = dense ? gsh + (uint32_t)(fo - fo0) : 4u * base_t;
     if (lane < kBloomGroup) {
       const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
       const uint64_t m_t = fastmod_magic(d_t);
       const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
-      slots[wv][lane] = make_uint4(base_t, d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
+      slots[wv][lane] = make_uint4(8u * byte_t, d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
       slot_c32[wv][lane] = c == d_t ? 0u : c;
     }
     const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
     for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
+    wave_phase();
+    if (dense && lane < g)  // each filter's k byte (util/bloom.cc:50), after its bits
+      reinterpret_cast<uint8_t*>(bm)[byte_t + (uint32_t)bytes] = (uint8_t)a.k;
     wave_phase();
     // the staging area: the region's free tail, less 48 B that a key's hash
     // may read past the span (none at all when the filters fill the region)
@@ -554,7 +570,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
       }
       const uint32_t j = pos - 1;
       const uint4 sl = slots[wv][j];
-      const uint32_t wbase = sl.x, d = sl.y;
+      const uint32_t bbase = sl.x, d = sl.y;
       const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;
       const uint32_t c32 = slot_c32[wv][j];
       const uint64_t s = kbase + oa0;
@@ -579,17 +595,35 @@ void bloom_build_kernel(BloomBuildArgs a) {
 #pragma unroll LSBM_PROBE_UNROLL
 #endif
       for (uint32_t q = 0; q < a.k; q++) {
-        atomicOr(&bm[wbase + (ps.pos >> 5)], 1u << (ps.pos & 31u));
+        const uint32_t b = bbase + ps.pos;
+        atomicOr(&bm[b >> 5], 1u << (b & 31u));
         ps.next();
       }
     }
     load_meta(grp + nwaves);
     wave_phase();
-    for (uint32_t j = 0; j < g; j++) {
-      const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + readlane64(fo, j);
-      const uint32_t nb = (uint32_t)readlane64(bytes, j);
-      store_window(dst, bm + __builtin_amdgcn_readlane(base_t, j), nb, lane);
-      if (lane == 0) *reinterpret_cast<gu8>(dst + nb) = (uint8_t)a.k;  // :50
+    if (dense) {
+      // LDS byte x <-> global byte dst0 - gsh + x, for x in [gsh, gsh + span):
+      // whole dwords as dword stores, the partial first / last dword as bytes
+      // (they share a dword with a neighbouring group's output)
+      const uint32_t end = gsh + (uint32_t)span;
+      const uint64_t gbase = dst0 - gsh;
+      for (uint32_t i = lane; i < (uint32_t)total; i += 64) {
+        if (4 * i >= gsh && 4 * i + 4 <= end) {
+          *reinterpret_cast<gu32>(gbase + 4ull * i) = bm[i];
+        } else {
+          const uint32_t v = bm[i];
+          for (uint32_t q = 0; q < 4; q++)
+            if (4 * i + q >= gsh && 4 * i + q < end) *reinterpret_cast<gu8>(gbase + 4ull * i + q) = (uint8_t)(v >> (8 * q));
+        }
+      }
+    } else {
+      for (uint32_t j = 0; j < g; j++) {
+        const uint64_t dst = reinterpret_cast<uint64_t>(a.out) + readlane64(fo, j);
+        const uint32_t nb = (uint32_t)readlane64(bytes, j);
+        store_window(dst, bm + __builtin_amdgcn_readlane(base_t, j), nb, lane);
+        if (lane == 0) *reinterpret_cast<gu8>(dst + nb) = (uint8_t)a.k;  // :50
+      }
     }
     wave_phase();
   }
