@@ -80,6 +80,34 @@ def test_oracle_length_and_bounds(snappy_oracle):
     assert snappy_oracle.uncompress(c, cap=299) == (False, b"")
 
 
+def test_lane_walk_model_matches_oracle(snappy_oracle, snappy_golden):
+    """The decoder's lane-parallel window walk (decode_lanes, restated in
+    tools/snappy_lanes_model.py) accepts and rejects exactly what the oracle
+    does, and writes the same bytes, on a subset of the fixture blocks, all
+    their corruptions and the crafted streams (the whole set: run the tool)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    from snappy_lanes_model import decode_lanes
+    n = 0
+    streams = []
+    for k, cs in enumerate(snappy_golden["cases"][:24:3]):
+        if cs["n"] > 0x3000:
+            continue
+        c = snappy_oracle.compress(block(cs["kind"], cs["n"], cs["seed"]))
+        streams.append(c)
+        streams.extend(m for _, m in mutations(c, 7000 + 3 * k))
+    streams.extend(crafted_bytes(r["name"], r) for r in snappy_golden["crafted"] if r["name"] != "literal_ext3")
+    for st in streams:
+        okp, ulen = snappy_oracle.uncompressed_length(st)
+        if not okp or ulen > 0x3000:
+            continue
+        i = 0
+        while st[i] >= 128:
+            i += 1
+        assert decode_lanes(st[i + 1:], ulen) == snappy_oracle.uncompress(st)
+        n += 1
+    assert n >= 40
+
+
 def test_snappy_entry_points_fail_loudly_without_device(product_lib):
     import torch
     if torch.cuda.is_available():
