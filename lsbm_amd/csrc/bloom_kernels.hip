@@ -637,10 +637,6 @@ __device__ __forceinline__ uint64_t load_le32(uint64_t p) {  // DecodeFixed32, a
 // util/bloom.cc:65-89 on the filter [f, f + len).
 __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_use) {
   if (len < 2) return false;
-  // `array[len-1] > k_use_`: a signed char converted to size_t
-  const uint64_t stored = (uint64_t)(int64_t)(int8_t)*reinterpret_cast<gcu8>(f + len - 1);
-  const uint64_t k = stored > k_use ? k_use : stored;
-  if (k > 30) return true;
   const uint64_t bits = (len - 1) * 8;
   const BitMod m = bit_mod(bits);
   const uint32_t delta = (h >> 17) | (h << 15);
@@ -654,14 +650,39 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
   }
   // The reference stops at the first clear bit (:85); the answer is the same
   // if a chunk of up to 16 probe bytes (all inside this filter) is requested
-  // at once and tested together: one round trip instead of up to k.
-  for (uint32_t j0 = 0; j0 < (uint32_t)k; j0 += 16) {
-    uint32_t v[16], bit[16];
+  // at once and tested together: one round trip instead of up to k.  The
+  // probe positions do not depend on the filter's stored k, so the first
+  // chunk (min(k_use, 16) probes) is requested together with the k byte:
+  // one round trip less per lookup (those past k are loaded and ignored).
+  const uint32_t k0n = k_use < 16 ? (uint32_t)k_use : 16u;
+  const uint8_t kb = *reinterpret_cast<gcu8>(f + len - 1);
+  uint32_t v[16], bit[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    bit[j] = 0u;
+    v[j] = 0u;
+    if ((uint32_t)j < k0n) {  // (k_use is the same in every lane)
+      const uint32_t bitpos = inc ? ps.pos : mod_bits(ps.h, m);
+      bit[j] = 1u << (bitpos & 7u);
+      v[j] = *reinterpret_cast<gcu8>(f + (bitpos >> 3));
+      if (inc) ps.next();
+      else ps.h += delta;
+    }
+  }
+  // `array[len-1] > k_use_`: a signed char converted to size_t
+  const uint64_t stored = (uint64_t)(int64_t)(int8_t)kb;
+  const uint64_t k = stored > k_use ? k_use : stored;
+  if (k > 30) return true;
+  bool all = true;
+#pragma unroll
+  for (int j = 0; j < 16; j++) all &= (uint32_t)j >= k || (v[j] & bit[j]) == bit[j];
+  if (!all) return false;
+  for (uint32_t j0 = k0n; j0 < (uint32_t)k; j0 += 16) {  // (k_use > 16 only)
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       bit[j] = 0u;
       v[j] = 0u;
-      if (j0 + j < (uint32_t)k) {  // (k is the same in every lane of a wave, in practice)
+      if (j0 + j < (uint32_t)k) {
         const uint32_t bitpos = inc ? ps.pos : mod_bits(ps.h, m);
         bit[j] = 1u << (bitpos & 7u);
         v[j] = *reinterpret_cast<gcu8>(f + (bitpos >> 3));
@@ -669,7 +690,6 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
         else ps.h += delta;
       }
     }
-    bool all = true;
 #pragma unroll
     for (int j = 0; j < 16; j++) all &= (v[j] & bit[j]) == bit[j];
     if (!all) return false;
@@ -696,10 +716,14 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     const bool act = q < a.n;
     uint64_t ks = reinterpret_cast<uint64_t>(a.keys), kn = 0;
     if (act) key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
+    // the filter handle (and data offset) do not depend on the hash: requested
+    // before it (the hash's LDS fences would otherwise hold them back)
+    const uint64_t qq = act ? q : 0;
+    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
+    const uint64_t size = a.handles[2 * qq + 1];
+    const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
     const uint32_t h = wave_hash(stg, kProbeStageWords * 4u - 48u, ks, kn, act);
     if (!act) continue;
-    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * q];
-    const uint64_t size = a.handles[2 * q + 1];
     bool may;
     if (a.mode == kProbeFilter) {
       may = key_may_match(c, size, h, a.k_use);
@@ -713,7 +737,7 @@ void bloom_probe_kernel(BloomProbeArgs a) {
         const uint64_t last_word = load_le32(c + size - 5);
         if (last_word <= size - 5) {
           const uint64_t num = (size - 5 - last_word) / 4;
-          const uint64_t index = a.data_offsets[q] >> (base_lg & 63u);
+          const uint64_t index = doff >> (base_lg & 63u);
           if (index < num) {
             const uint64_t start = load_le32(c + last_word + index * 4);
             const uint64_t limit = load_le32(c + last_word + index * 4 + 4);

@@ -11,7 +11,7 @@ for pass in 1 2; do
   for v in default ${VARIANTS:-bprev}; do
     if [ $v = default ]; then L=""; else L="build/abl/lib_$v.so"; fi
     echo "== $v pass $pass" >> gpurun_out/bloom_ab.log
-    LSBM_LIB_PATH=$L timeout -k 10 300 python -u tools/bench_bloom.py build --cpu-filters 0 >> gpurun_out/bloom_ab.log 2>&1 || exit 1
+    LSBM_LIB_PATH=$L timeout -k 10 300 python -u tools/bench_bloom.py ${WHICH:-build} --cpu-filters 0 >> gpurun_out/bloom_ab.log 2>&1 || exit 1
   done
 done
-grep -E "==|bloom_build" gpurun_out/bloom_ab.log | cut -c1-220
+grep -E "==|bloom_" gpurun_out/bloom_ab.log | cut -c1-220
