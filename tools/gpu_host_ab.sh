@@ -1,5 +1,5 @@
 # Host-layer A/B on one box: SealTables with and without its host trailer
-# writes (LSBM_DIAG_SEAL_NO_WRITE, diagnostic), two interleaved passes.
+# writes (LSBM_DIAG_SEAL_NO_WRITE: a temporary diagnostic build, not in the product).
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for pass in 1 2; do
