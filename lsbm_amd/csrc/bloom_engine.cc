@@ -18,7 +18,7 @@ namespace lsbm {
 hipError_t launch_bloom_build(const BloomBuildArgs& a, int grid, hipStream_t stream);
 hipError_t launch_bloom_probe(const BloomProbeArgs& a, int grid, hipStream_t stream);
 int bloom_build_blocks_per_cu();
-int bloom_probe_blocks_per_cu();
+int bloom_probe_blocks_per_cu(uint32_t mode);
 
 namespace {
 
@@ -52,7 +52,7 @@ int probe(const uint8_t* base, const uint64_t* handles, const uint64_t* data_off
   a.strip = strip;
   a.mode = mode;
   // grid-stride: no more workgroups than are resident at once
-  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, bloom_probe_blocks_per_cu()),
+  const hipError_t e = launch_bloom_probe(a, grid_for(cus, n, 256, bloom_probe_blocks_per_cu(mode)),
                                           static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "bloom_probe_kernel");
 }

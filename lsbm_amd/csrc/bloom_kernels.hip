@@ -699,31 +699,83 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
 
 constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 31-B keys + slack)
 
-#ifdef LSBM_PROBE_WAVES_PER_EU  // A/B builds only
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSBM_PROBE_WAVES_PER_EU)))
-#else
-__global__ __launch_bounds__(256)
+// One instantiation per mode (the other mode's code dropped).  The
+// one-filter-per-query probe is held to 6 waves per SIMD (<= 80 VGPRs, a few
+// spilled outside the probe loop): 0.504 -> 0.491 ms against the 5 waves its
+// 90 VGPRs allow; the filter-block probe, whose spills would sit in its
+// offset-array lookups, ran 0.61 -> 0.82 ms under the same bound and keeps
+// its registers (profiles/r02/bloom/ab_probe_pipelined.log).
+#ifndef LSBM_PROBE_WAVES_PER_EU  // (A/B builds override)
+#define LSBM_PROBE_WAVES_PER_EU 6
 #endif
+template <uint32_t kMode>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(kMode == kProbeFilter ? LSBM_PROBE_WAVES_PER_EU : 1)))
 void bloom_probe_kernel(BloomProbeArgs a) {
+  a.mode = kMode;  // compile-time: the other mode's code is dropped
   __shared__ __attribute__((aligned(16))) uint32_t stage[4][kProbeStageWords];
   uint32_t* stg = stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t hits = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   // wave-uniform rounds of 64 consecutive queries (the hash is a wave operation)
-  for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q0 < a.n; q0 += stride) {
+#ifndef LSBM_PROBE_NO_PIPELINE  // A/B builds only
+  // Pipelined like the build: a round's key offsets are loaded two rounds
+  // ahead and its staged key words (16-B chunks in registers) one round
+  // ahead, so no round waits for its keys.
+  const uint64_t kbase = reinterpret_cast<uint64_t>(a.keys);
+  const uint64_t safe = reinterpret_cast<uint64_t>(a.key_offsets) & ~15ull;  // a readable 16-B chunk
+  const uint32_t avail = kProbeStageWords * 4u - 48u;
+  const uint64_t q00 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  uint64_t oa0 = 0, oa1 = 0, ob0 = 0, ob1 = 0;
+  if (q00 + lane < a.n) load_off2(a.key_offsets, q00 + lane, oa0, oa1);
+  if (q00 + stride + lane < a.n) load_off2(a.key_offsets, q00 + stride + lane, ob0, ob1);
+  SpanPlan plan;
+  u32x4 ch0, ch1;
+  {
+    const bool act = q00 + lane < a.n;
+    const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
+    plan = plan_span(kbase + oa0, n, avail, safe);
+    fetch_span(plan, ch0, ch1);
+  }
+  for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
-    uint64_t ks = reinterpret_cast<uint64_t>(a.keys), kn = 0;
-    if (act) key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
+    const uint64_t ks = kbase + oa0;
+    const uint64_t kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
     // the filter handle (and data offset) do not depend on the hash: requested
     // before it (the hash's LDS fences would otherwise hold them back)
     const uint64_t qq = act ? q : 0;
     const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
     const uint64_t size = a.handles[2 * qq + 1];
     const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
+    // this round's chunks go to LDS; the next round's plan and loads go out
+    const SpanPlan cur = plan;
+    const u32x4 cc0 = ch0, cc1 = ch1;
+    {
+      const bool act1 = q + stride < a.n;
+      const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
+      plan = plan_span(kbase + ob0, n1, avail, safe);
+      fetch_span(plan, ch0, ch1);
+      oa0 = ob0;
+      oa1 = ob1;
+      if (q + 2 * stride < a.n) load_off2(a.key_offsets, q + 2 * stride, ob0, ob1);
+    }
+    const uint32_t h = staged_hash(stg, cur, cc0, cc1, ks, kn, act);
+    if (!act) continue;
+#else
+  for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q0 < a.n; q0 += stride) {
+    const uint64_t q = q0 + lane;
+    const bool act = q < a.n;
+    uint64_t ks = reinterpret_cast<uint64_t>(a.keys), kn = 0;
+    if (act) key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
+    const uint64_t qq = act ? q : 0;
+    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
+    const uint64_t size = a.handles[2 * qq + 1];
+    const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
     const uint32_t h = wave_hash(stg, kProbeStageWords * 4u - 48u, ks, kn, act);
     if (!act) continue;
+#endif
     bool may;
     if (a.mode == kProbeFilter) {
       may = key_may_match(c, size, h, a.k_use);
@@ -767,7 +819,10 @@ hipError_t launch_bloom_build(const BloomBuildArgs& a, int grid, hipStream_t str
 }
 
 hipError_t launch_bloom_probe(const BloomProbeArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(bloom_probe_kernel, dim3(grid), dim3(256), 0, stream, a);
+  if (a.mode == kProbeFilter)
+    hipLaunchKernelGGL(bloom_probe_kernel<kProbeFilter>, dim3(grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(bloom_probe_kernel<kProbeFilterBlock>, dim3(grid), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -790,16 +845,17 @@ int bloom_build_blocks_per_cu() {
   return v;
 }
 
-int bloom_probe_blocks_per_cu() {
+int bloom_probe_blocks_per_cu(uint32_t mode) {
 #ifdef LSBM_PROBE_WGS  // A/B builds only
   return LSBM_PROBE_WGS;
 #endif
-  static const int v = [] {
+  auto query = [](const void* k) {
     int b = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, bloom_probe_kernel, 256, 0) == hipSuccess &&
-                       b > 0 ? b : 4;
-  }();
-  return v;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0) == hipSuccess && b > 0 ? b : 4;
+  };
+  static const int v0 = query(reinterpret_cast<const void*>(bloom_probe_kernel<kProbeFilter>));
+  static const int v1 = query(reinterpret_cast<const void*>(bloom_probe_kernel<kProbeFilterBlock>));
+  return mode == kProbeFilter ? v0 : v1;
 }
 
 }  // namespace lsbm
