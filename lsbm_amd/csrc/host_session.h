@@ -70,8 +70,14 @@ struct Stage {
 
 class HostSession {
  public:
-  static constexpr int kStages = 3;
-  static constexpr size_t kChunkBytes = 64u << 20;  // bulk bytes per stage and chunk (at most)
+#ifndef LSBM_HOST_STAGES  // (A/B builds override)
+#define LSBM_HOST_STAGES 3
+#endif
+#ifndef LSBM_HOST_CHUNK_MB
+#define LSBM_HOST_CHUNK_MB 64
+#endif
+  static constexpr int kStages = LSBM_HOST_STAGES;
+  static constexpr size_t kChunkBytes = (size_t)LSBM_HOST_CHUNK_MB << 20;  // bulk bytes per stage and chunk (at most)
   static constexpr size_t kMinChunkBytes = 4u << 20;
   // Chunk size for a job of `total` bytes: about a quarter of it, so that even
   // one table's copy, DMA and kernel overlap, within [4 MiB, 64 MiB].
