@@ -672,11 +672,19 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
         t[4] = (uint8_t)(pend_v >> 24);
       } else if constexpr (mode == kModeLogSeal) {
         if (args.file) {  // (null: the masked crcs only, lsbm_log_crcs_dev)
+#ifndef LSBM_LOG_BYTE_STORES  // A/B builds only
+          // header[0..4) as one unaligned dword store (gfx950 global memory
+          // takes any byte alignment) instead of four byte stores: every store
+          // sits in the vmcnt queue in front of the next rounds' row loads
+          typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
+          *reinterpret_cast<gu32u>(pend_a) = pend_v;
+#else
           uint8_t* h = reinterpret_cast<uint8_t*>(pend_a);
           h[0] = (uint8_t)pend_v;
           h[1] = (uint8_t)(pend_v >> 8);
           h[2] = (uint8_t)(pend_v >> 16);
           h[3] = (uint8_t)(pend_v >> 24);
+#endif
         }
         if (args.out) args.out[b_lo + pend_i] = pend_v;
       } else if constexpr (mode == kModeOut || mode == kModeSstCrc) {
