@@ -566,6 +566,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
   u32x4 pshift = {0, 0, 0, 0}, pfin = {0, 0, 0, 0};
   uint32_t paux0 = 0, paux1 = 0;
+  (void)paux1;  // (two-load A/B builds only)
   uint64_t pk = 0, pb = 0, pat = 0;
   bool pact = false, plast = false, pfits = true, pfast = false;
 
@@ -648,10 +649,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       if constexpr (mode == kModeVerify)
         good = ((args.flags & 1u) ? mask_crc(crc) : crc) == paux0;
       else  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+#ifndef LSBM_VERIFY_TWO_LOADS
+        good = pfits && unmask_crc(paux0) == crc;
+#else
         good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
+#endif
 #ifdef LSBM_DIAG_VERIFY_WRITEBACK  // diagnostic builds only: rewrite the stored crc bytes
       if (pfits && li < 4)
-        reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(unaligned_word(paux0, paux1, pat) >> (8 * li));
+        reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(paux0 >> (8 * li));
 #endif
       if (mine) {
         pend_a = reinterpret_cast<uint64_t>(args.ok + pb);
@@ -1004,10 +1009,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       } else if constexpr (mode == kModeSstSeal || mode == kModeSstCrc) {
         q0 = need ? reinterpret_cast<uint64_t>(args.types + pb) : dummy;
       } else if constexpr (mode == kModeSstVerify || mode == kModeLogVerify) {
+#ifndef LSBM_VERIFY_TWO_LOADS  // A/B builds only
+        // the stored crc [pat, pat + 4) as one unaligned dword load
+        q0 = need ? pat : dummy;
+#else
         // the dwords holding bytes pat and pat + 3 (one dword when aligned:
         // never a byte past the stored crc)
         q0 = need ? (pat & ~3ull) : dummy;
         q1 = need ? ((pat + 3) & ~3ull) : dummy;
+#endif
       }
       asm volatile("" : "+v"(q0), "+v"(q1));
       if constexpr (mode == kModeSstSeal || mode == kModeSstCrc) {
@@ -1015,8 +1025,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       } else if constexpr (mode == kModeVerify) {
         paux0 = *reinterpret_cast<gptr_u32>(q0);
       } else if constexpr (mode == kModeSstVerify || mode == kModeLogVerify) {
+#ifndef LSBM_VERIFY_TWO_LOADS
+        typedef const __attribute__((address_space(1), aligned(1))) uint32_t* gptr_u32u;
+        paux0 = *reinterpret_cast<gptr_u32u>(q0);
+#else
         paux0 = *reinterpret_cast<gptr_u32>(q0);
         paux1 = *reinterpret_cast<gptr_u32>(q1);
+#endif
       }
     }
     rj = rn;
