@@ -18,6 +18,7 @@ namespace lsbm {
 hipError_t launch_snappy_length(const SnapLenArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress_large(const SnapEncArgs& a, int grid, hipStream_t stream);
 
@@ -98,12 +99,15 @@ __attribute__((visibility("default"))) int lsbm_snappy_uncompress_dev(
   a.n_bad = d_n_bad;
   a.n = n;
   // pass 1: blocks that fit a small LDS slice; pass 2: the ones it deferred
-  // (ok = 2), scanned 64 per wave
+  // (ok = 2), scanned 64 per wave, in 16 KiB slices; pass 3: what pass 2
+  // deferred (ok = 3), in 64 KiB slices or against global memory
   const hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e = launch_snappy_uncompress(a, wave_grid(cus, n, kSnapDecWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_kernel");
   e = launch_snappy_uncompress_large(a, wave_grid(cus, (n + 63) / 64, kSnapDecLargeWgsPerCu), s);
-  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_uncompress_large_kernel");
+  if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_deferred_kernel (16 KiB)");
+  e = launch_snappy_uncompress_huge(a, wave_grid(cus, (n + 63) / 64, kSnapDecHugeWgsPerCu), s);
+  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_uncompress_deferred_kernel (64 KiB)");
 }
 
 }  // extern "C"

@@ -326,9 +326,11 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 // window; or from an LDS copy (A/B builds).  Same accept / reject decisions as
 // decode() (tests/test_snappy.py; tools/snappy_lanes_model.py restates the
 // walk and checks it against the oracle).
-template <bool kGlobalIn>
+template <bool kGlobalIn, bool kBig = false>
 __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
-  constexpr uint32_t kLenCap = 0x4000u;  // > any valid length here (ulen < the 16 KiB slice)
+  // > any valid length here: ulen < the slice (16 KiB; kBig: 64 KiB, where a
+  // tag's size and output length no longer pack into one 32-bit word)
+  constexpr uint32_t kLenCap = kBig ? 0x10000u : 0x4000u;
   uint32_t op = 0;    // output offset of the next tag
   uint32_t next = 0;  // input position of the next tag
   // a literal's data [lit_lo, lit_hi) that runs into later windows; out[lit_out] <- in[lit_lo]
@@ -374,7 +376,8 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     const uint32_t len = kind == 0 ? len_lit : (kind == 1 ? 4 + ((c >> 2) & 7u) : len0);
     const uint32_t off = kind == 1 ? ((c >> 5) << 8) | xm : xm;
     const uint32_t lenc = len < kLenCap ? len : kLenCap;
-    const uint32_t ws = (hdr + (kind == 0 ? lenc : 0u)) | (lenc << 16);  // size | output length
+    const uint32_t size = hdr + (kind == 0 ? lenc : 0u);
+    const uint32_t ws = kBig ? size : size | (lenc << 16);  // size | output length
     // 2. the real tags of this window and their output offsets (from op)
     uint64_t real = 0;
     uint32_t opt = 0, opa = 0;
@@ -387,8 +390,13 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
       // gfx9's constant bus takes one SGPR besides M0)
       asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(opt) : "s"(opa), "s"(s) : "m0");
       const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ws, (int)s);
-      opa += v >> 16;
-      s += v & 0xffffu;
+      if constexpr (kBig) {
+        opa += (uint32_t)__builtin_amdgcn_readlane((int)lenc, (int)s);
+        s += v;
+      } else {
+        opa += v >> 16;
+        s += v & 0xffffu;
+      }
     }
     const uint32_t o = op + opt;
     if (real) {
@@ -420,13 +428,13 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     if (real) {  // the last tag's literal data may run into the next windows
       const uint32_t t = 63u - (uint32_t)__builtin_clzll(real);
       const uint32_t tp = (uint32_t)__builtin_amdgcn_readlane((int)pack, (int)t);
-      const uint32_t tw = (uint32_t)__builtin_amdgcn_readlane((int)ws, (int)t);
+      const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)(kBig ? lenc : ws >> 16), (int)t);
       lit_lo = ip + t + ((tp >> 2) & 7u);
-      lit_hi = (tp & 3u) == 0 ? lit_lo + (tw >> 16) : lit_lo;
+      lit_hi = (tp & 3u) == 0 ? lit_lo + tl : lit_lo;
       lit_out = op + (tp >> 12);
     }
     // 5. the copies, in order: output [dst, dst + len) from [dst - off, ...)
-    const uint32_t cpa = o | ((len - 1) << 16);  // (a valid copy: o < 2^14, len <= 64)
+    const uint32_t cpa = o | ((len - 1) << 16);  // (a valid copy: o < 2^16, len <= 64)
     const uint32_t cps = o - off;
     uint64_t cm = real & __ballot(kind != 0);
     while (cm) {
@@ -455,7 +463,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
 // LSBM_SNAP_STAGED_INPUT stage them in the slice too), else
 // (kGlobalFallback) against global memory.  Returns 2 when the block neither
 // fits nor may fall back.
-template <uint32_t kSlice, bool kGlobalFallback>
+template <uint32_t kSlice, bool kGlobalFallback, uint32_t kDefer = 2>
 __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint64_t b, uint32_t lane
                                                      SNAP_STAMPS_PARAM) {
   const uint64_t s = a.offsets[b], e = a.offsets[b + 1];
@@ -487,7 +495,7 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     ok = decode_lanes<false>(lds_in, cl, win, ulen, lane);
 #else
     uint8_t* win = smem;
-    ok = decode_lanes<true>(g, cl, win, ulen, lane);
+    ok = decode_lanes<true, (kSlice > 16384)>(g, cl, win, ulen, lane);
 #endif
     SNAP_STAMP(2);
 #ifndef LSBM_SNAP_DIAG_NO_OUT  // diagnostic build only (tools/snappy_diag.py): skips the output, wrong results
@@ -496,7 +504,7 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     SNAP_STAMP(3);
     wave_phase();
   } else if (!kGlobalFallback) {
-    return 2;
+    return kDefer;
   } else {
     ok = decode<false>(g, cl, a.out + os, ulen, lane);
   }
@@ -529,20 +537,25 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_kernel(SnapDec
 #endif
 }
 
-// Pass 2: the blocks pass 1 deferred, found 64 at a time by ballot, in a
-// large slice or against global memory.
-__global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_large_kernel(SnapDecArgs a) {
+// Passes 2 and 3: the blocks the pass before deferred (ok = kPending), found
+// 64 at a time by ballot.  Pass 2: 16 KiB output windows (10 waves per CU),
+// deferring what does not fit (ok = 3); pass 3: 64 KiB windows (2 waves per
+// CU), the rest serially against global memory (decode<false>).  (Before
+// pass 3, blocks of 16-64 KiB went straight to the serial path: 8.6 GB/s on
+// 62 KB db_bench-like blocks, profiles/r02/snappy/merge_blocks.log.)
+template <uint32_t kSlice, uint32_t kPending, bool kFallback>
+__global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_deferred_kernel(SnapDecArgs a) {
   const uint32_t lane = threadIdx.x;
   for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
     const uint64_t i = c + lane;
-    uint64_t pend = __ballot(i < a.n && a.ok[i] == 2);
+    uint64_t pend = __ballot(i < a.n && a.ok[i] == kPending);
     while (pend) {
       const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
       pend &= pend - 1;
 #ifdef LSBM_SNAP_STAMPS
       Stamps sa = {};
 #endif
-      record(a, b, uncompress_block<kSnapDecLdsLarge, true>(a, b, lane SNAP_STAMPS_ARG), lane);
+      record(a, b, uncompress_block<kSlice, kFallback, kPending + 1>(a, b, lane SNAP_STAMPS_ARG), lane);
     }
   }
 }
@@ -902,8 +915,14 @@ hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t 
 }
 
 hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(snappy_uncompress_large_kernel, dim3(grid), dim3(kSnapThreads), kSnapDecLdsLarge,
-                     stream, a);
+  hipLaunchKernelGGL((snappy_uncompress_deferred_kernel<kSnapDecLdsLarge, 2, false>), dim3(grid),
+                     dim3(kSnapThreads), kSnapDecLdsLarge, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((snappy_uncompress_deferred_kernel<kSnapDecLdsHuge, 3, true>), dim3(grid),
+                     dim3(kSnapThreads), kSnapDecLdsHuge, stream, a);
   return hipGetLastError();
 }
 

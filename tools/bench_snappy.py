@@ -163,10 +163,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--cpu-sample", type=int, default=65536)
+    ap.add_argument("--merge", type=int, default=1,
+                    help="(diagnostic) concatenate this many consecutive blocks into one: larger blocks")
     args = ap.parse_args()
 
     buf, offs_h = make_blocks(args.blocks)
-    n = args.blocks
+    if args.merge > 1:
+        offs_h = np.ascontiguousarray(np.concatenate([offs_h[:-1:args.merge], offs_h[-1:]]))
+    n = offs_h.size - 1
     # the CPU baseline first, in forked worker processes, before this process
     # touches the GPU (no child ever holds a device context)
     # (--cpu-seconds 0: no CPU baseline, e.g. under rocprofv3 --pmc, whose
