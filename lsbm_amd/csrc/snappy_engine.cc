@@ -20,6 +20,7 @@ hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t 
 hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream);
+hipError_t launch_snappy_compress_mid(const SnapEncArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress_large(const SnapEncArgs& a, int grid, hipStream_t stream);
 
 namespace {
@@ -58,10 +59,13 @@ __attribute__((visibility("default"))) int lsbm_snappy_compress_dev(
   a.out_offsets = d_out_offsets;
   a.out_len = d_out_len;
   a.n = n;
-  // pass 1: one-fragment blocks that fit a 22 KiB LDS slice; pass 2: the ones
-  // it deferred (out_len = kSnapDeferred), scanned 64 per wave
+  // pass 1: one-fragment blocks that fit a 22 KiB LDS slice; the middle pass:
+  // the ones it deferred (out_len = kSnapDeferred, scanned 64 per wave) that
+  // fit 48 KiB; the last pass: the rest, the table in LDS, the bytes in global
   hipError_t e = launch_snappy_compress(a, wave_grid(cus, n, kSnapEncWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_compress_kernel");
+  e = launch_snappy_compress_mid(a, wave_grid(cus, (n + 63) / 64, kSnapEncMidWgsPerCu), s);
+  if (e != hipSuccess) return engine_fail_hip(e, "snappy_compress_mid_kernel");
   e = launch_snappy_compress_large(a, wave_grid(cus, (n + 63) / 64, kSnapEncLargeWgsPerCu), s);
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_compress_large_kernel");
 }

@@ -866,6 +866,46 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_kernel(SnapEncAr
 #endif
 }
 
+// Middle pass: deferred blocks of one fragment whose table and bytes fit a
+// 48 KiB slice (up to ~16 KiB: a 2^14-entry table and the fragment in LDS,
+// 3 waves per CU), the same code as pass 1; the rest stay deferred for the
+// last pass.  (Without it every block past pass 1's 22 KiB slice went to the
+// last pass, 2 waves per CU with the fragment read from global memory:
+// profiles/r02/snappy/merge_blocks.log.)
+__global__ __launch_bounds__(kSnapThreads) void snappy_compress_mid_kernel(SnapEncArgs a) {
+  const uint32_t lane = threadIdx.x;
+  const EncWave w = enc_wave(reinterpret_cast<uint32_t*>(smem + kSnapEncMidSlice), lane);
+#ifdef LSBM_SNAP_STAMPS
+  Stamps sa = {};
+  sa.t = __builtin_amdgcn_s_memtime();
+#endif
+  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+    const uint64_t i = c + lane;
+    uint64_t pend = __ballot(i < a.n && a.out_len[i] == kSnapDeferred);
+    while (pend) {
+      const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t s = a.offsets[b];
+      const uint64_t len = a.offsets[b + 1] - s;
+      if (len > kSnapFragment) continue;  // (pass 1 handled lengths >= 2^32)
+      const uint32_t n = (uint32_t)len;
+      const uint32_t tsize = table_size_for(n);
+      if (2 * tsize + n + 4 > kSnapEncMidSlice) continue;  // + the staged copy's last dword
+      uint8_t* const out = a.out + a.out_offsets[b];
+      const uint64_t op = write_preamble(out, n, lane);
+      uint16_t* table = reinterpret_cast<uint16_t*>(smem);
+      uint8_t* lin = smem + 2 * tsize;
+      for (uint32_t j = lane; j < tsize / 8; j += 64) reinterpret_cast<uint4*>(smem)[j] = make_uint4(0, 0, 0, 0);
+      stage_to_lds(lin, a.base + s, n, lane);
+      wave_phase();
+      const uint64_t end = compress_fragment<true>(lin, n, table, tsize, out, op, lane, w.off32, w.sk32, w.off64,
+                                                   w.sk64, w.buckets SNAP_STAMPS_ARG);
+      wave_phase();
+      if (lane == 0) a.out_len[b] = end;
+    }
+  }
+}
+
 // Pass 2: the deferred blocks, found 64 at a time by ballot, fragment by
 // 64 KiB fragment: the hash table (up to 2^15 entries, 64 KiB) in LDS, the
 // fragment bytes read from global memory.  No global scratch.
@@ -928,6 +968,11 @@ hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStre
 
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(kSnapThreads), kSnapEncLds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_compress_mid(const SnapEncArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(snappy_compress_mid_kernel, dim3(grid), dim3(kSnapThreads), kSnapEncMidLds, stream, a);
   return hipGetLastError();
 }
 

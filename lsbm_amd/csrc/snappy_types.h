@@ -33,6 +33,10 @@ constexpr uint32_t kSnapDecLdsHuge = 65536;  // pass 3: blocks of 16-64 KiB
 constexpr uint32_t kSnapEncSlice = 22528;
 constexpr uint32_t kSnapEncBuckets = 512;
 constexpr uint32_t kSnapEncLds = kSnapEncSlice + kSnapEncBuckets;
+// the encoder's middle pass: 48 KiB per wave (a 2^14-entry table and up to
+// ~16 KiB of fragment), 3 waves per CU
+constexpr uint32_t kSnapEncMidLds = 48 * 1024;
+constexpr uint32_t kSnapEncMidSlice = kSnapEncMidLds - kSnapEncBuckets;
 #ifndef LSBM_SNAP_PROBES
 #define LSBM_SNAP_PROBES 24
 #endif
@@ -48,6 +52,7 @@ constexpr uint32_t kSnapEncWgsPerCu = 160 * 1024 / kSnapEncLds;
 // LDS (2^15 entries), fragment bytes from global memory; 2 waves per CU
 constexpr uint32_t kSnapEncLargeLds = 2 * kSnapMaxTable + kSnapEncBuckets;
 constexpr uint32_t kSnapEncLargeWgsPerCu = 160 * 1024 / kSnapEncLargeLds;
+constexpr uint32_t kSnapEncMidWgsPerCu = 160 * 1024 / kSnapEncMidLds;
 constexpr uint64_t kSnapDeferred = ~0ull - 1;  // out_len of a block left for pass 2
 
 struct SnapLenArgs {
