@@ -17,8 +17,7 @@ namespace lsbm {
 // launchers (snappy_kernels.hip)
 hipError_t launch_snappy_length(const SnapLenArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t stream);
-hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream);
-hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_snappy_uncompress_deferred(const SnapDecArgs& a, int tier, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress_mid(const SnapEncArgs& a, int grid, hipStream_t stream);
 hipError_t launch_snappy_compress_large(const SnapEncArgs& a, int grid, hipStream_t stream);
@@ -64,9 +63,9 @@ __attribute__((visibility("default"))) int lsbm_snappy_compress_dev(
   // fit 48 KiB; the last pass: the rest, the table in LDS, the bytes in global
   hipError_t e = launch_snappy_compress(a, wave_grid(cus, n, kSnapEncWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_compress_kernel");
-  e = launch_snappy_compress_mid(a, wave_grid(cus, (n + 63) / 64, kSnapEncMidWgsPerCu), s);
+  e = launch_snappy_compress_mid(a, wave_grid(cus, (n + kSnapDecScan - 1) / kSnapDecScan, kSnapEncMidWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_compress_mid_kernel");
-  e = launch_snappy_compress_large(a, wave_grid(cus, (n + 63) / 64, kSnapEncLargeWgsPerCu), s);
+  e = launch_snappy_compress_large(a, wave_grid(cus, (n + kSnapDecScan - 1) / kSnapDecScan, kSnapEncLargeWgsPerCu), s);
   return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_compress_large_kernel");
 }
 
@@ -102,16 +101,18 @@ __attribute__((visibility("default"))) int lsbm_snappy_uncompress_dev(
   a.ok = d_ok;
   a.n_bad = d_n_bad;
   a.n = n;
-  // pass 1: blocks that fit a small LDS slice; pass 2: the ones it deferred
-  // (ok = 2), scanned 64 per wave, in 16 KiB slices; pass 3: what pass 2
-  // deferred (ok = 3), in 64 KiB slices or against global memory
+  // pass 1: blocks that fit a small LDS slice; passes 2-5: the ones the pass
+  // before deferred (ok = 2 .. 5), scanned 16 per wave, in 9, 17, 33 and 80
+  // KiB slices, the last one decoding what is left against global memory
   const hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e = launch_snappy_uncompress(a, wave_grid(cus, n, kSnapDecWgsPerCu), s);
   if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_kernel");
-  e = launch_snappy_uncompress_large(a, wave_grid(cus, (n + 63) / 64, kSnapDecLargeWgsPerCu), s);
-  if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_deferred_kernel (16 KiB)");
-  e = launch_snappy_uncompress_huge(a, wave_grid(cus, (n + 63) / 64, kSnapDecHugeWgsPerCu), s);
-  return e == hipSuccess ? LSBM_OK : engine_fail_hip(e, "snappy_uncompress_deferred_kernel (64 KiB)");
+  for (int t = 0; t < kSnapDecTiers; t++) {
+    e = launch_snappy_uncompress_deferred(a, t, wave_grid(cus, (n + kSnapDecScan - 1) / kSnapDecScan,
+                                                          (int)(160 * 1024 / kSnapDecTierLds[t])), s);
+    if (e != hipSuccess) return engine_fail_hip(e, "snappy_uncompress_deferred_kernel");
+  }
+  return LSBM_OK;
 }
 
 }  // extern "C"

@@ -328,9 +328,9 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 // walk and checks it against the oracle).
 template <bool kGlobalIn, bool kBig = false>
 __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ulen, uint32_t lane) {
-  // > any valid length here: ulen < the slice (16 KiB; kBig: 64 KiB, where a
+  // > any valid length here: ulen < the slice (16 KiB; kBig: 80 KiB, where a
   // tag's size and output length no longer pack into one 32-bit word)
-  constexpr uint32_t kLenCap = kBig ? 0x10000u : 0x4000u;
+  constexpr uint32_t kLenCap = kBig ? 0x20000u : 0x4000u;
   uint32_t op = 0;    // output offset of the next tag
   uint32_t next = 0;  // input position of the next tag
   // a literal's data [lit_lo, lit_hi) that runs into later windows; out[lit_out] <- in[lit_lo]
@@ -434,7 +434,8 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
       lit_out = op + (tp >> 12);
     }
     // 5. the copies, in order: output [dst, dst + len) from [dst - off, ...)
-    const uint32_t cpa = o | ((len - 1) << 16);  // (a valid copy: o < 2^16, len <= 64)
+    constexpr uint32_t kOB = kBig ? 17u : 16u;  // bits of a valid copy's output offset (o < ulen)
+    const uint32_t cpa = o | ((len - 1) << kOB);  // (len <= 64)
     const uint32_t cps = o - off;
     uint64_t cm = real & __ballot(kind != 0);
     while (cm) {
@@ -443,7 +444,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
       cm &= cm - 1;
       const uint32_t ta = (uint32_t)__builtin_amdgcn_readlane((int)cpa, (int)t);
       const uint32_t src = (uint32_t)__builtin_amdgcn_readlane((int)cps, (int)t);
-      const uint32_t dst = ta & 0xffffu, tlen = (ta >> 16) + 1;
+      const uint32_t dst = ta & ((1u << kOB) - 1u), tlen = (ta >> kOB) + 1;
       // byte j of the copy is out[src + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it
       if (lane < tlen) {
@@ -495,7 +496,7 @@ __device__ __forceinline__ uint32_t uncompress_block(const SnapDecArgs& a, uint6
     ok = decode_lanes<false>(lds_in, cl, win, ulen, lane);
 #else
     uint8_t* win = smem;
-    ok = decode_lanes<true, (kSlice > 16384)>(g, cl, win, ulen, lane);
+    ok = decode_lanes<true, (kSlice > 16384)>(g, cl, win, ulen, lane);  // (kBig: ulen >= 16 KiB possible)
 #endif
     SNAP_STAMP(2);
 #ifndef LSBM_SNAP_DIAG_NO_OUT  // diagnostic build only (tools/snappy_diag.py): skips the output, wrong results
@@ -537,18 +538,23 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_kernel(SnapDec
 #endif
 }
 
-// Passes 2 and 3: the blocks the pass before deferred (ok = kPending), found
-// 64 at a time by ballot.  Pass 2: 16 KiB output windows (10 waves per CU),
-// deferring what does not fit (ok = 3); pass 3: 64 KiB windows (2 waves per
-// CU), the rest serially against global memory (decode<false>).  (Before
-// pass 3, blocks of 16-64 KiB went straight to the serial path: 8.6 GB/s on
-// 62 KB db_bench-like blocks, profiles/r02/snappy/merge_blocks.log.)
+// Passes 2-5: the blocks the pass before deferred (ok = kPending), found 64
+// at a time by ballot, in 9 / 17 / 33 / 80 KiB output windows (17 / 9 / 4 / 2
+// waves per CU: blocks of 8, 16, 32 and 64 KiB block sizes, which run a little
+// over), each deferring what does not fit (ok = kPending + 1) and the last
+// decoding the rest serially against global memory (decode<false>).  (With a
+// 16 KiB pass only, blocks of 16-64 KiB went straight to the serial path:
+// 8.6 GB/s on 62 KB db_bench-like blocks, profiles/r02/snappy/merge_blocks.log.)
 template <uint32_t kSlice, uint32_t kPending, bool kFallback>
 __global__ __launch_bounds__(kSnapThreads) void snappy_uncompress_deferred_kernel(SnapDecArgs a) {
   const uint32_t lane = threadIdx.x;
-  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+  // 16 blocks per scan, so that a batch of larger blocks (all deferred) still
+  // gives every wave slot of the pass work: 64 per scan left 8 of 17 waves
+  // per CU busy on 8 KB blocks
+  constexpr uint32_t kScan = kSnapDecScan;
+  for (uint64_t c = (uint64_t)blockIdx.x * kScan; c < a.n; c += (uint64_t)gridDim.x * kScan) {
     const uint64_t i = c + lane;
-    uint64_t pend = __ballot(i < a.n && a.ok[i] == kPending);
+    uint64_t pend = __ballot(lane < kScan && i < a.n && a.ok[i] == kPending);
     while (pend) {
       const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
       pend &= pend - 1;
@@ -879,9 +885,9 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_mid_kernel(SnapE
   Stamps sa = {};
   sa.t = __builtin_amdgcn_s_memtime();
 #endif
-  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+  for (uint64_t c = (uint64_t)blockIdx.x * kSnapDecScan; c < a.n; c += (uint64_t)gridDim.x * kSnapDecScan) {
     const uint64_t i = c + lane;
-    uint64_t pend = __ballot(i < a.n && a.out_len[i] == kSnapDeferred);
+    uint64_t pend = __ballot(lane < kSnapDecScan && i < a.n && a.out_len[i] == kSnapDeferred);
     while (pend) {
       const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
       pend &= pend - 1;
@@ -917,9 +923,9 @@ __global__ __launch_bounds__(kSnapThreads) void snappy_compress_large_kernel(Sna
   Stamps sa = {};
   sa.t = __builtin_amdgcn_s_memtime();
 #endif
-  for (uint64_t c = (uint64_t)blockIdx.x * 64; c < a.n; c += (uint64_t)gridDim.x * 64) {
+  for (uint64_t c = (uint64_t)blockIdx.x * kSnapDecScan; c < a.n; c += (uint64_t)gridDim.x * kSnapDecScan) {
     const uint64_t i = c + lane;
-    uint64_t pend = __ballot(i < a.n && a.out_len[i] == kSnapDeferred);
+    uint64_t pend = __ballot(lane < kSnapDecScan && i < a.n && a.out_len[i] == kSnapDeferred);
     while (pend) {
       const uint64_t b = c + (uint64_t)__builtin_ctzll(pend);
       pend &= pend - 1;
@@ -954,16 +960,29 @@ hipError_t launch_snappy_uncompress(const SnapDecArgs& a, int grid, hipStream_t 
   return hipGetLastError();
 }
 
-hipError_t launch_snappy_uncompress_large(const SnapDecArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((snappy_uncompress_deferred_kernel<kSnapDecLdsLarge, 2, false>), dim3(grid),
-                     dim3(kSnapThreads), kSnapDecLdsLarge, stream, a);
+// the deferred decode passes, in order (snappy_types.h kSnapDecTierLds)
+template <int kTier>
+hipError_t launch_deferred_tier(const SnapDecArgs& a, int grid, hipStream_t stream) {
+  constexpr uint32_t lds = kSnapDecTierLds[kTier];
+  constexpr bool last = kTier + 1 == kSnapDecTiers;
+  auto* k = snappy_uncompress_deferred_kernel<lds, 2 + kTier, last>;
+  if (lds > 65536) {  // above the default dynamic limit, within gfx950's 160 KiB per workgroup
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kSnapThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-hipError_t launch_snappy_uncompress_huge(const SnapDecArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((snappy_uncompress_deferred_kernel<kSnapDecLdsHuge, 3, true>), dim3(grid),
-                     dim3(kSnapThreads), kSnapDecLdsHuge, stream, a);
-  return hipGetLastError();
+hipError_t launch_snappy_uncompress_deferred(const SnapDecArgs& a, int tier, int grid, hipStream_t stream) {
+  static_assert(kSnapDecTiers == 4, "one case per tier");
+  switch (tier) {
+    case 0: return launch_deferred_tier<0>(a, grid, stream);
+    case 1: return launch_deferred_tier<1>(a, grid, stream);
+    case 2: return launch_deferred_tier<2>(a, grid, stream);
+    default: return launch_deferred_tier<3>(a, grid, stream);
+  }
 }
 
 hipError_t launch_snappy_compress(const SnapEncArgs& a, int grid, hipStream_t stream) {

@@ -25,8 +25,11 @@ constexpr uint32_t kSnapThreads = 64;
 #endif
 #endif
 constexpr uint32_t kSnapDecLds = LSBM_SNAP_DEC_LDS;
-constexpr uint32_t kSnapDecLdsLarge = 16384;
-constexpr uint32_t kSnapDecLdsHuge = 65536;  // pass 3: blocks of 16-64 KiB
+// the deferred passes' slices (output window only): for blocks of the 8, 16,
+// 32 and 64 KiB block sizes (which run a little over)
+constexpr uint32_t kSnapDecTierLds[4] = {9216, 17408, 33792, 81920};
+constexpr int kSnapDecTiers = 4;
+constexpr uint32_t kSnapDecScan = 16;  // blocks per ballot scan in the deferred passes, decoder and encoder (<= 64)
 // encoder: hash table (2 B/entry) + fragment bytes in a 22 KiB slice (a
 // 4 KiB block with its 8,192-entry table needs 20.1 KiB), then the match
 // search's hash-bucket counters (one byte each): 22.5 KiB, 7 waves per CU
@@ -45,8 +48,7 @@ constexpr uint32_t kSnapMaxTableBits = 15;             // libsnappy >= 1.1.10 (o
 constexpr uint32_t kSnapMaxTable = 1u << kSnapMaxTableBits;
 constexpr uint32_t kSnapFragment = 65536;              // snappy kBlockSize
 constexpr uint32_t kSnapDecWgsPerCu = 160 * 1024 / kSnapDecLds;  // LDS-limited residency
-constexpr uint32_t kSnapDecLargeWgsPerCu = 160 * 1024 / kSnapDecLdsLarge;
-constexpr uint32_t kSnapDecHugeWgsPerCu = 160 * 1024 / kSnapDecLdsHuge;
+
 constexpr uint32_t kSnapEncWgsPerCu = 160 * 1024 / kSnapEncLds;
 // encoder pass 2 (blocks that pass 1 cannot hold): the largest hash table in
 // LDS (2^15 entries), fragment bytes from global memory; 2 waves per CU
