@@ -708,9 +708,12 @@ constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 3
 #ifndef LSBM_PROBE_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_WAVES_PER_EU 6
 #endif
+#ifndef LSBM_PROBE_BLOCK_WAVES_PER_EU  // (A/B builds override)
+#define LSBM_PROBE_BLOCK_WAVES_PER_EU 1
+#endif
 template <uint32_t kMode>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(kMode == kProbeFilter ? LSBM_PROBE_WAVES_PER_EU : 1)))
+__attribute__((amdgpu_waves_per_eu(kMode == kProbeFilter ? LSBM_PROBE_WAVES_PER_EU : LSBM_PROBE_BLOCK_WAVES_PER_EU)))
 void bloom_probe_kernel(BloomProbeArgs a) {
   a.mode = kMode;  // compile-time: the other mode's code is dropped
   __shared__ __attribute__((aligned(16))) uint32_t stage[4][kProbeStageWords];
