@@ -158,6 +158,9 @@ __device__ __forceinline__ Raw8 issue8(const uint8_t* p, uint32_t i, uint32_t n)
 
 __device__ __forceinline__ uint64_t finish8(Raw8 r) { return r.v >> r.sh; }
 
+// 4 bytes at p[i] (the encoder's callers only ask for bytes inside the
+// fragment).  Global memory: one unaligned dword load (gfx950 global loads
+// take any byte alignment).
 template <bool kLds>
 __device__ __forceinline__ uint32_t load32(const uint8_t* p, uint32_t i) {
   if (kLds) {
@@ -165,8 +168,8 @@ __device__ __forceinline__ uint32_t load32(const uint8_t* p, uint32_t i) {
     const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
     return (uint32_t)(v >> (8 * (i & 3u)));
   } else {
-    return (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
-           ((uint32_t)p[i + 3] << 24);
+    typedef const __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
+    return *reinterpret_cast<gu32u>(reinterpret_cast<uint64_t>(p) + i);
   }
 }
 
