@@ -382,7 +382,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     const uint32_t size = hdr + (kind == 0 ? lenc : 0u);
     const uint32_t ws = kBig ? size : size | (lenc << 16);  // size | output length
     // 2. the real tags of this window and their output offsets (from op)
-#ifdef LSBM_SNAP_BALLOT_MASK  // A/B builds only
+#ifndef LSBM_SNAP_SCALAR_MASK  // (A/B builds: the mask built by two scalar ops per tag, 4% slower)
     // the real tags are the lanes the walk writes: opt starts at ~0 (never a
     // real tag's offset) and the mask is one ballot after the walk, not two
     // scalar ops per tag
@@ -394,7 +394,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     uint32_t s = next - ip;
     const uint32_t lim = cl - ip;
     while (s < 64u && s < lim) {
-#ifndef LSBM_SNAP_BALLOT_MASK
+#ifdef LSBM_SNAP_SCALAR_MASK
       real |= 1ull << s;
 #endif
       // opt[s] = opa: v_writelane (one VALU instead of a compare and a select;
@@ -410,7 +410,7 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
         s += v & 0xffffu;
       }
     }
-#ifdef LSBM_SNAP_BALLOT_MASK
+#ifndef LSBM_SNAP_SCALAR_MASK
     const uint64_t real = __ballot(opt != ~0u);
 #endif
     const uint32_t o = op + opt;
