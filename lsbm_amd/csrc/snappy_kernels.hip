@@ -450,20 +450,21 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     }
     // 5. the copies, in order: output [dst, dst + len) from [dst - off, ...)
     constexpr uint32_t kOB = kBig ? 17u : 16u;  // bits of a valid copy's output offset (o < ulen)
-    const uint32_t cpa = o | ((len - 1) << kOB);  // (len <= 64)
+    // packed per copy: output offset | (len - 1) << kOB | overlapping (off < len) << 23
+    const uint32_t cpa = o | ((len - 1) << kOB) | (off < len ? 1u << 23 : 0u);  // (len <= 64)
     const uint32_t cps = o - off;
     uint64_t cm = real & __ballot(kind != 0);
     while (cm) {
       wave_order();
       const uint32_t t = (uint32_t)__builtin_ctzll(cm);
-      cm &= cm - 1;
+      cm ^= 1ull << t;
       const uint32_t ta = (uint32_t)__builtin_amdgcn_readlane((int)cpa, (int)t);
       const uint32_t src = (uint32_t)__builtin_amdgcn_readlane((int)cps, (int)t);
-      const uint32_t dst = ta & ((1u << kOB) - 1u), tlen = (ta >> kOB) + 1;
+      const uint32_t dst = ta & ((1u << kOB) - 1u), tlen = ((ta >> kOB) & 63u) + 1;
       // byte j of the copy is out[src + j mod off]: an overlapping copy
       // (off < len) repeats its first off bytes, all written before it
       if (lane < tlen) {
-        const uint32_t k = src + tlen <= dst ? lane : lane_mod(lane, dst - src);
+        const uint32_t k = (ta >> 23) & 1u ? lane_mod(lane, dst - src) : lane;
         out[dst + lane] = out[src + k];
       }
     }
