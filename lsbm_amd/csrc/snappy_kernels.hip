@@ -417,13 +417,15 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     if (real) {
       // 3. every real tag's checks (a literal's extra length bytes past the
       // stream are hdr > rem, like a copy's offset bytes)
-      const bool me = (real >> lane) & 1u;
-      const uint32_t rem = cl - (ip + lane);
-      // (bitwise, not short-circuit: no divergent branches)
-      const bool bad_lit = len > rem - hdr;
-      const bool bad_cp = (off == 0) | (off > o);
-      const bool bad = (hdr > rem) | (len > ulen - o) | ((kind == 0) ? bad_lit : bad_cp);
-      if (__ballot(me && bad)) return false;
+      const uint32_t rem = cl - (ip + lane);  // >= 1 on a real tag's lane
+      // the kind's own test as one compare ka >= kb: a literal's data past the
+      // stream (len > rem - hdr; rem - hdr + 1 wraps only when hdr > rem,
+      // which fails anyway), a copy's offset 0 or before the output
+      // (off - 1 >= o).  Bitwise, not short-circuit: no divergent branches.
+      const uint32_t ka = kind == 0 ? len : off - 1u;
+      const uint32_t kb = kind == 0 ? rem - hdr + 1u : o;
+      const bool bad = (hdr > rem) | (len > ulen - o) | (ka >= kb);
+      if (__ballot(bad) & real) return false;
     }
     // 4. literal bytes: the tag owning this lane's byte (the last real tag at
     // or before it) and its data range, or the literal carried in

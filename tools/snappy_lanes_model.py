@@ -65,10 +65,9 @@ def decode_lanes(inp, ulen):
             c, kind, hdr, ln, off = lanes[t]
             rem = (cl - (ip + t)) & M32
             o = (op + opt[t]) & M32
-            if kind == 0:
-                bad = hdr > rem or ln > ((rem - hdr) & M32) or ln > ((ulen - o) & M32)
-            else:
-                bad = hdr > rem or off == 0 or off > o or ln > ((ulen - o) & M32)
+            ka = ln if kind == 0 else (off - 1) & M32  # the kind's own test: ka >= kb
+            kb = (rem - hdr + 1) & M32 if kind == 0 else o
+            bad = hdr > rem or ln > ((ulen - o) & M32) or ka >= kb
             if bad:
                 return False, b""
         for l in range(64):  # literal bytes
