@@ -433,13 +433,11 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
     const uint64_t below = real & upto;
     const uint32_t own = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
     const uint32_t po = (uint32_t)__shfl((int)pack, (int)own);
-    uint32_t dlo = lit_lo, dhi = lit_hi, dout = lit_out;
-    if (below) {
-      const uint32_t d0 = ip + own + ((po >> 2) & 7u);
-      dlo = d0;
-      dhi = (po & 3u) == 0 ? d0 + ((po >> 5) & 127u) : d0;  // (a copy owns no data)
-      dout = op + (po >> 12);
-    }
+    // (selects, not a branch: below is 0 only on lanes before the window's first tag)
+    const uint32_t d0 = ip + own + ((po >> 2) & 7u);
+    const uint32_t d1 = (po & 3u) == 0 ? d0 + ((po >> 5) & 127u) : d0;  // (a copy owns no data)
+    const bool hb = below != 0;
+    const uint32_t dlo = hb ? d0 : lit_lo, dhi = hb ? d1 : lit_hi, dout = hb ? op + (po >> 12) : lit_out;
     const uint32_t pos = ip + lane;
     if (pos >= dlo && pos < dhi) out[dout + (pos - dlo)] = (uint8_t)c;
     if (real) {  // the last tag's literal data may run into the next windows
