@@ -306,7 +306,8 @@ __device__ bool decode(const uint8_t* in, uint32_t cl, uint8_t* out, uint32_t ul
 //     kind, header size, length, offset).
 //  2. A scalar walk over the real tags of the window (one readlane of each
 //     tag's size and length) marks them in a 64-bit mask and hands each its
-//     output offset (v_writelane): two scalar adds per tag.
+//     output offset (v_writelane): one scalar add per tag (an inline-asm
+//     loop of 7 instructions; blocks of 16 KiB and more: the C loop).
 //  3. Every real tag is checked at once against the conditions RawUncompress
 //     tests (header or literal past the stream, offset 0 or before the output,
 //     output past ulen).  The decode fails iff one of them fails: the tags up
@@ -393,6 +394,37 @@ __device__ bool decode_lanes(const uint8_t* in, uint32_t cl, uint8_t* out, uint3
 #endif
     uint32_t s = next - ip;
     const uint32_t lim = cl - ip;
+#if !defined(LSBM_SNAP_SCALAR_MASK) && !defined(LSBM_SNAP_C_WALK)
+    if constexpr (!kBig) {
+      // the walk as 7 instructions per tag: one scalar accumulator
+      // acc = opa << 16 | s (s < 2^16; opa < 2^16 up to the first tag whose
+      // output passes ulen < 16 KiB, which fails its check) advanced by one
+      // add of the packed size | output length; the lane select is acc's low
+      // half in M0; each real lane receives acc (opa in its high half)
+      // (readfirstlane: both are wave-uniform; it tells the compiler so)
+      const uint32_t lim64 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lim < 64u ? lim : 64u));
+      uint32_t acc = (uint32_t)__builtin_amdgcn_readfirstlane((int)s), v;
+      asm volatile(
+          "s_and_b32 m0, %[acc], 0xffff\n\t"
+          "s_cmp_lt_u32 m0, %[lim]\n\t"
+          "s_cbranch_scc0 2f\n"
+          "1:\n\t"
+          "v_writelane_b32 %[opt], %[acc], m0\n\t"
+          "v_readlane_b32 %[v], %[ws], m0\n\t"
+          "s_add_u32 %[acc], %[acc], %[v]\n\t"
+          "s_and_b32 m0, %[acc], 0xffff\n\t"
+          "s_cmp_lt_u32 m0, %[lim]\n\t"
+          "s_cbranch_scc1 1b\n"
+          "2:"
+          : [acc] "+s"(acc), [opt] "+v"(opt), [v] "=&s"(v)
+          : [ws] "v"(ws), [lim] "s"(lim64)
+          : "m0", "scc");
+      (void)v;
+      s = acc & 0xffffu;
+      opa = acc >> 16;
+      opt = opt == ~0u ? opt : opt >> 16;
+    } else
+#endif
     while (s < 64u && s < lim) {
 #ifdef LSBM_SNAP_SCALAR_MASK
       real |= 1ull << s;
