@@ -119,21 +119,22 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v) {
 
 // Copy the prebuilt LDS image (DevConsts::lds_image) into LDS: every thread
 // issues all of its 16-B loads before its first LDS write (one round trip).
+template <uint32_t kThreads = kBlockThreads>
 __device__ __forceinline__ void load_lds_tables(uint32_t* lds, const DevConsts* __restrict__ dc) {
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
   constexpr uint32_t kChunks = kLdsBytes / 16;
-  constexpr uint32_t kPer = (kChunks + kBlockThreads - 1) / kBlockThreads;
+  constexpr uint32_t kPer = (kChunks + kThreads - 1) / kThreads;
   const v4* __restrict__ src = reinterpret_cast<const v4*>(dc->lds_image);
   v4* dst = reinterpret_cast<v4*>(lds);
   v4 t[kPer];
 #pragma unroll
   for (uint32_t k = 0; k < kPer; k++) {
-    const uint32_t i = threadIdx.x + k * kBlockThreads;
+    const uint32_t i = threadIdx.x + k * kThreads;
     if (i < kChunks) t[k] = src[i];
   }
 #pragma unroll
   for (uint32_t k = 0; k < kPer; k++) {
-    const uint32_t i = threadIdx.x + k * kBlockThreads;
+    const uint32_t i = threadIdx.x + k * kThreads;
     if (i < kChunks) dst[i] = t[k];
   }
   __syncthreads();

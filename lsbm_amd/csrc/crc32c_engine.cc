@@ -31,6 +31,7 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
                         const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
                         const DevConsts* dc, int grid, hipStream_t stream);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
+bool ragged_uses_stream(const RaggedArgs& a);
 hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint32_t* bounds, int grid,
                                hipStream_t stream);
 hipError_t launch_trailer_scatter(uint8_t* file, uint64_t limit, const uint64_t* handles, const uint8_t* types,
@@ -99,6 +100,12 @@ void build_consts(DevConsts* c) {
   for (uint32_t i = 0; i < kRowPowTables; i++)  // A^(128 * 2^i) = A^(2^(7+i))
     memcpy(&c->lds_image[kNibRowPow / 4 + i * 128], c->pow_nib[7 + i], 512);
   memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
+  for (uint32_t lo = 0, t = 0; lo <= 16; lo++)  // stream kernel: bytes [lo, hi) of a 16-B chunk
+    for (uint32_t hi = lo; hi <= 16; hi++, t++)
+      for (uint32_t b = 0; b < 16; b++)
+        if (b >= lo && b < hi) c->lds_image[kStreamHM / 4 + t * 4 + b / 4] |= 0xffu << (8 * (b % 4));
+  for (uint32_t d = 0; d < 128; d++)  // stream kernel: ~0 injected d bytes before the row start
+    c->lds_image[kStreamR0 / 4 + d] = gf2::apply(gf2::byte_pow(-(int64_t)d), 0xffffffffu);
   memset(c->zero16, 0, sizeof(c->zero16));
   // column forms for the units kernel: A^(128 k) and A^e, e = -127 .. 1
   {
@@ -214,7 +221,8 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
   a.u_noinit = u_noinit();
   a.bounds = nullptr;
   a.nchunks = 0;
-  const uint64_t nwaves = (uint64_t)st->num_cus * kWavesPerWg;
+  const uint64_t nwaves =
+      (uint64_t)st->num_cus * (ragged_uses_stream(a) ? kStreamWavesPerWg : kWavesPerWg);
   // (LSBM_SWEEP_CHUNK_BLOCKS: A/B runs only; 0 = no chunked sweep)
   static const uint64_t chunk_blocks = [] {
     const char* v = getenv("LSBM_SWEEP_CHUNK_BLOCKS");

@@ -1,0 +1,590 @@
+// crc32c_stream.hip -- the stream-major CRC-32C kernel for densely packed
+// images: SSTable files, WAL / MANIFEST log images, offsets[] batches.
+//
+// The units kernel (crc32c_units.h) gives each 8-lane group one unit of one
+// block per round and runs the round in lock-step for as many rows as its
+// longest unit.  On short or uneven blocks most of its loads read the zero
+// pad (343 B of 1,024 B per wave-load on WAL records, 691 B on config 4) and
+// the round overhead is paid per ~10 rows.  Here the rows of the image are
+// streamed regardless of block boundaries:
+//
+//   * a wave takes a piece of consecutive blocks (as the units kernel) and
+//     cuts it into sub-pieces of at most 256 blocks, whose extents it loads
+//     into registers (4 per lane) and checks: ascending and non-overlapping
+//     (s_j >= e_{j-1}), within a 2 GiB window.  A sub-piece that is not goes
+//     through the units walk instead (any order, any overlap);
+//   * the sub-piece's rows [floor(s_first / 128), last row] are cut into 8
+//     segments of Q rows, one per lane group, and every group streams its
+//     segment row after row with the fixed kernel's access pattern: one 16-B
+//     load per lane per 128-B row through a buffer descriptor bounded to the
+//     sub-piece (chunks outside it read zeros), the braids c_m = A^128(c_m)
+//     ^ w_m (util/crc32c.cc:295-302 for a 128-B stride);
+//   * a row that holds a block boundary of its group takes the slow path:
+//     the bytes of the row that belong to the open block are kept (a 16-B
+//     mask from LDS), the block's braids are saved into a slot when it ends,
+//     the next block starts from zero braids with its init register ~0
+//     injected as A^-(s mod 128)(~0) at the row start (an LDS table), so that
+//     the register is exactly ~0 when its first byte is absorbed (:289);
+//   * every kR rows the slots are merged (merge_braids, lock-step over the
+//     groups) and finished: A^-z (z = the bytes after e in its last row), the
+//     mode (CRC, masked CRC, verify, SSTable trailer CRC / check, log header
+//     seal / check), results parked in lanes and written 8 per group at once;
+//   * a block that crosses into the next group's segment leaves its braids
+//     there at the segment end (T); the group where it ends saves the rest
+//     (its head).  At the sub-piece end T pieces are merged, shifted to the
+//     block's last row by A^(128 k), summed per block by a segmented xor-scan
+//     over the groups and added to the head before it is finished.
+//
+// Every row is read once per wave and fully used: no pad loads, no per-round
+// lock-step.  Results are those of crc32c::Extend(~0-init) over each block
+// (util/crc32c.cc:286-329), exactly as the units kernel computes them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_units.h"
+
+namespace lsbm {
+
+constexpr uint32_t kSubBlocks = 64;   // blocks per sub-piece: one extent per lane
+constexpr uint32_t kSlots = 2;        // block ends saved per group between flushes
+constexpr int kStreamAux = 2;         // buffer-load policy: non-temporal (read once)
+constexpr uint32_t kBank = 3;         // rows per load bank (two in flight); round-2 A/B on the
+                                      // fixed kernel: 3-6 rows per bank alike
+
+typedef const __attribute__((address_space(1), aligned(1))) uint32_t* gptr_u32u;
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32);
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
+  return (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)v, d) |
+         ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d) << 32);
+}
+// Last row of block [s, e) (relative byte offsets): the row of byte e - 1, or
+// of s for an empty block.
+__device__ __forceinline__ uint32_t end_row(uint32_t s, uint32_t e) {
+  return e > s ? (e - 1u) >> 7 : s >> 7;
+}
+
+// A block of 2 GiB or more: the units walk over the wave's range, out of
+// line (its registers are not the stream loop's).
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
+__device__ __attribute__((noinline)) void units_fallback(RaggedArgs args, uint64_t wave, uint64_t nwaves,
+                                                         uint64_t b0, uint64_t b1, bool chunked,
+                                                         uint32_t pi, uint32_t p_end) {
+  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b0, b1, chunked, pi, p_end, false);
+}
+
+template <uint32_t kR, uint32_t kMode, uint32_t kExt>
+__global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArgs args) {
+  static_assert(kR % 8 == 0 && kR <= 32, "rows per step: banks of 4");
+  args.mode = kMode;
+  args.extents = kExt;
+  constexpr bool kSstModes = kMode == kModeSstVerify || kMode == kModeSstCrc;
+  constexpr uint32_t kFallbackRows = kSstModes ? kSstUnitRows : LSBM_UNIT_ROWS;
+  // group state bits (fl)
+  constexpr uint32_t kOpen = 1u, kHeadSeg = 2u, kIdle = 4u, kHValid = 16u;
+  const DevConsts* __restrict__ dc = args.dc;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t g = lane >> 3, li = lane & 7u;
+  const uint32_t lb = (lane & 31u) << 2;
+  const uint32_t L0 = lb, L1 = lb | 0x80u, L2 = lb | 0x10000u, L3 = lb | 0x10080u;
+  const uint32_t lane_fin = kNibFin | lb;
+  const uint64_t wave = (uint64_t)blockIdx.x * kStreamWavesPerWg +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kStreamWavesPerWg;
+  bool chunked;
+  uint32_t pi, p_end;
+  uint64_t b_lo, b_hi;
+  wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
+  const uint32_t* __restrict__ bnd = args.bounds;
+  if (chunked) {
+    b_lo = bnd[pi];
+    b_hi = bnd[pi + 1];
+  }
+  load_lds_tables<kStreamThreads>(g_lds, dc);
+  const uint64_t base = reinterpret_cast<uint64_t>(args.base);
+  const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
+  const char* lds_c = reinterpret_cast<const char*>(g_lds);
+
+  // ---- results: parked one per lane, written 8 per group at once ----
+  uint32_t pend_i = ~0u;  // this lane's parked block (~0 = none; n < 2^32 - 1)
+  uint64_t pend_h = 0;    // (log seal: its header)
+  uint32_t pend_v = 0;
+  uint32_t npark = 0;     // results parked in this group
+  uint32_t nbad = 0;      // (lane 0 of each group)
+  (void)pend_h;
+  auto store_parked = [&]() {
+    if (pend_i != ~0u) {
+      if constexpr (kMode == kModeLogSeal) {
+        if (args.file) {  // header[0..4): one unaligned dword store
+          typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
+          *reinterpret_cast<gu32u>(pend_h) = pend_v;
+        }
+        if (args.out) args.out[pend_i] = pend_v;
+      } else if constexpr (kMode == kModeOut || kMode == kModeSstCrc) {
+        args.out[pend_i] = pend_v;
+      } else {
+        args.ok[pend_i] = (uint8_t)pend_v;
+      }
+    }
+    pend_i = ~0u;
+    npark = 0;
+  };
+
+  const uint64_t r_lo = b_lo, r_hi = b_hi;  // (the range, for the fallback)
+  const uint32_t pi0 = pi;
+  bool huge = false;  // a block of >= 2 GiB: the units walk redoes this wave's range
+  for (;;) {  // pieces (one, or this wave's range of every chunk)
+    for (uint64_t b0 = b_lo; b0 < b_hi;) {
+      // ---- the next sub-piece: up to 64 blocks in order (s_j >= e_{j-1}) ----
+      const uint32_t navail = b_hi - b0 < kSubBlocks ? (uint32_t)(b_hi - b0) : kSubBlocks;
+      uint32_t sr, er;  // relative to pb; er carries bit 31 for a record that does not fit
+      uint64_t pb, desc;
+      uint32_t nrec, NR, nb;
+      {
+        const bool vq = lane < navail;
+        const uint64_t bj = vq ? b0 + lane : b0;
+        ExtRaw rq = load_ext_raw(args, bj);
+        if constexpr (kExt == kExtLogHeaders) log_length(args, rq);
+        uint64_t sa, ea, at;
+        bool fits;
+        extent_from_raw(args, bj, rq, sa, ea, fits, at);
+        // a record that does not fit is empty and bad; a well-formed batch
+        // has such records only at its end, where the image ends
+        if (!fits) sa = ea = base + args.limit;
+        const uint64_t s_first = readlane64(sa, 0);
+        pb = s_first & ~127ull;  // the sub-piece's row base (absolute, 128-aligned)
+        // The sub-piece ends before the first block that is not in order (or
+        // overlaps the one before; offsets that go back make an empty block
+        // and then an earlier start) or that reaches 2 GiB past pb.
+        const uint64_t pe = shfl_up64(ea, 1);
+        bool cut = !vq || ea - pb >= (1ull << 31) - 256u;
+        if (lane > 0) cut = cut || sa < pe;
+        const uint64_t cm = __ballot(cut);
+        nb = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
+        nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)nb);
+        if (nb == 0u) {  // the first block alone spans >= 2 GiB
+          huge = true;
+          b0 += 1;
+          continue;
+        }
+        const uint64_t e_last = readlane64(ea, nb - 1u), s_last = readlane64(sa, nb - 1u);
+        desc = pb + ((uint32_t)(s_first - pb) & ~15u);  // chunks in [desc, roundup16(e_last)) are read
+        nrec = (uint32_t)(((e_last + 15u) & ~15ull) - desc);
+        sr = lane < nb ? (uint32_t)(sa - pb) : 0x7fffff00u;
+        er = lane < nb ? (uint32_t)(ea - pb) | (fits ? 0u : 0x80000000u) : 0x7fffff00u;
+        NR = end_row((uint32_t)(s_last - pb), (uint32_t)(e_last - pb)) + 1u;
+      }
+      // (wave-uniform: readfirstlane keeps the descriptor in SGPRs, with no
+      // waterfall loop around the loads)
+      desc = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)desc) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(desc >> 32)) << 32);
+      nrec = (uint32_t)__builtin_amdgcn_readfirstlane((int)nrec);
+      pb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pb) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pb >> 32)) << 32);
+      NR = (uint32_t)__builtin_amdgcn_readfirstlane((int)NR);
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(desc), (short)0, (int)nrec, 0x00020000);
+      const uint32_t Q = (NR + 7u) >> 3;  // rows per segment
+      const uint32_t seg0 = g * Q;        // this group's first row (relative to pb)
+      // the first block of this group's segment: the number of blocks that end before it
+      uint32_t cur = 0;
+      {
+        const uint32_t re = end_row(sr, er & 0x7fffffffu);
+#pragma unroll
+        for (uint32_t gg = 1; gg < 8; gg++) {
+          const uint32_t f = (uint32_t)__builtin_popcountll(__ballot(lane < nb && re < gg * Q));
+          cur = g == gg ? f : cur;
+        }
+      }
+
+      // ---- the group's window: lane li holds block (cur - wi) + li ----
+      // (a block past the sub-piece never starts or ends)
+      uint32_t wi = 0;
+      uint32_t ws = (uint32_t)__shfl((int)sr, (int)((cur + li) & 63u));
+      uint32_t we = (uint32_t)__shfl((int)er, (int)((cur + li) & 63u));
+      if (cur + li >= nb) ws = we = 0x7fffff00u;
+      // the current block [cs, ce) (relative to pb)
+      uint32_t cs = (uint32_t)__shfl((int)ws, (int)(g * 8u));
+      uint32_t ce = (uint32_t)__shfl((int)we, (int)(g * 8u)) & 0x7fffffffu;
+      uint32_t fl = 0;
+      if (cur >= nb) fl |= kIdle | kOpen;
+      else if ((cs >> 7) < seg0) fl |= kOpen | kHeadSeg;  // continued from the previous segment
+      const uint32_t first = cur;
+      // the next row that needs the slow path: the current block's last row,
+      // its first row, the next row (a gap: no block open), never (idle)
+      auto next_ev = [&](uint32_t rr) -> uint32_t {
+        return (fl & kIdle) ? ~0u : ((fl & kOpen) ? end_row(cs, ce) : min(cs >> 7, rr + 1u));
+      };
+      uint32_t ev = next_ev(seg0 - 1u);
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      // saved block ends: braids and block (relative to b0)
+      uint32_t cnt = 0;
+      uint32_t sx0[4] = {0, 0, 0, 0}, sx1[4] = {0, 0, 0, 0};
+      uint32_t sb0 = 0, sb1 = 0;
+      uint32_t hv = 0;  // the raw CRC of the head block (block `first`, continued from the previous segment)
+
+      // Finish block b0 + j for this group (act: group-uniform); every lane
+      // executes it (cols_apply sums over the group; the extents come from the
+      // lane that loaded them).  X = the block's raw CRC at the end of its
+      // last row.
+      auto finish = [&](bool act, uint32_t X, uint32_t j) {
+        const uint32_t bs = (uint32_t)__shfl((int)sr, (int)(j & 63u));
+        const uint32_t bw = (uint32_t)__shfl((int)er, (int)(j & 63u));
+        const uint32_t be = bw & 0x7fffffffu;
+        const uint32_t bi = (uint32_t)b0 + j;
+        const bool bad = (bw >> 31) != 0u;
+        const bool empty = bs == be;
+        const uint32_t z = (0u - be) & 127u;  // bytes of the last row after e (pb is 128-aligned)
+        // A^-z, or A^(1-z) when the type byte follows (WriteRawBlock's Extend)
+        uint32_t fi = kMode == kModeSstCrc ? 128u - z : 127u - z;
+        fi = act ? fi : 127u;
+        const u32x4 cols =
+            *reinterpret_cast<gptr_u32x4>(reinterpret_cast<uint64_t>(&dc->fin_cols[fi][4 * li]));
+        // the stored / written checksum: after the type byte, or the log header
+        // (6 bytes before the record's CRC bytes: it may lie before pb)
+        const uint64_t at = kMode == kModeSstVerify ? pb + be : pb + bs - 6u;
+        uint64_t q = dummy;
+        if constexpr (kMode == kModeVerify) q = act ? reinterpret_cast<uint64_t>(args.expect + bi) : dummy;
+        if constexpr (kMode == kModeSstCrc) q = act ? reinterpret_cast<uint64_t>(args.types + bi) : dummy;
+        if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify) q = act && !bad ? at : dummy;
+        asm volatile("" : "+v"(q));
+        uint32_t aux = 0;
+        if constexpr (kMode == kModeVerify) aux = *reinterpret_cast<gptr_u32>(q);
+        if constexpr (kMode == kModeSstCrc) aux = *reinterpret_cast<gptr_u8>(q);
+        if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify)
+          aux = *reinterpret_cast<gptr_u32u>(q);
+        uint32_t l = cols_apply(cols, X, li);
+        // an empty block leaves the init register ~0 (advanced by the type byte's slot)
+        if (empty) l = kMode == kModeSstCrc ? advance_byte(0xffffffffu) : 0xffffffffu;
+        const uint32_t crc = l ^ 0xffffffffu;
+        uint32_t val;
+        bool put = act;
+        if constexpr (kMode == kModeOut) {
+          val = (args.flags & 1u) ? mask_crc(crc) : crc;
+        } else if constexpr (kMode == kModeVerify) {
+          const bool good = ((args.flags & 1u) ? mask_crc(crc) : crc) == aux;
+          if (act && !good && li == 0) nbad++;
+          val = good ? 1u : 0u;
+        } else if constexpr (kMode == kModeSstCrc) {  // table/table_builder.cc:245-249
+          if (act && bad && li == 0) nbad++;
+          val = bad ? 0u : mask_crc((l ^ advance_byte(aux & 0xffu)) ^ 0xffffffffu);
+        } else if constexpr (kMode == kModeLogSeal) {  // common/log_writer.cc:85-88
+          if (act && bad && li == 0) {
+            if (args.out) args.out[bi] = 0;
+            nbad++;
+          }
+          put = act && !bad;
+          val = mask_crc(crc);
+        } else {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+          const bool good = !bad && unmask_crc(aux) == crc;
+          if (act && !good && li == 0) nbad++;
+          val = good ? 1u : 0u;
+        }
+        // park it in lane (npark mod 8) of the group
+        if (__ballot(put && npark == 8u) != 0ull) store_parked();
+        if (put && li == (npark & 7u)) {
+          pend_i = bi;
+          pend_v = val;
+          if constexpr (kMode == kModeLogSeal) pend_h = at;
+        }
+        npark += put ? 1u : 0u;
+      };
+      auto flush = [&]() {  // every lane active: merge and finish the saved blocks
+#pragma unroll 1
+        for (uint32_t j = 0; j < kSlots; j++) {
+          if (__ballot(cnt > j) == 0ull) break;
+          const uint32_t X = merge_braids(g_lds, j ? sx1[0] : sx0[0], j ? sx1[1] : sx0[1],
+                                          j ? sx1[2] : sx0[2], j ? sx1[3] : sx0[3], lane_fin);
+          const uint32_t bj = j ? sb1 : sb0;
+          const bool v = cnt > j;
+          const bool hd = v && bj == first && (fl & kHeadSeg);  // the segment's continued block
+          if (hd) {
+            hv = X;
+            fl |= kHValid;
+          }
+          finish(v && !hd, X, bj);
+        }
+        cnt = 0;
+      };
+      static_assert(kSlots == 2, "two slots");
+      // Save braids x of the block cur, which ends in this row, into the
+      // group's next slot (ends: group-uniform; the caller made room).
+      auto save = [&](bool ends, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+        if (ends && cnt == 0u) {
+          sx0[0] = x0;
+          sx0[1] = x1;
+          sx0[2] = x2;
+          sx0[3] = x3;
+          sb0 = cur;
+        }
+        if (ends && cnt == 1u) {
+          sx1[0] = x0;
+          sx1[1] = x1;
+          sx1[2] = x2;
+          sx1[3] = x3;
+          sb1 = cur;
+        }
+        cnt += ends ? 1u : 0u;
+      };
+      // The bytes [lo, hi) of this lane's chunk (0 <= lo <= hi <= 16), and the
+      // init register of a block that starts in this row at s (inject): the
+      // block's contribution to the row's braids.
+      auto part = [&](u32x4 w, uint32_t lo, uint32_t hi, bool inject, uint32_t s, uint32_t& x0,
+                      uint32_t& x1, uint32_t& x2, uint32_t& x3) {
+        const uint32_t t = lo * 17u - ((lo * (lo - 1u)) >> 1) + hi - lo;  // (lo = 0: hi)
+        const u32x4 m = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + t * 16u);
+        x0 ^= w.x & m.x;
+        x1 ^= w.y & m.y;
+        x2 ^= w.z & m.z;
+        x3 ^= w.w & m.w;
+        if (inject && li == 0u)  // the init register, d = s mod 128 bytes before s
+          x0 ^= *reinterpret_cast<const uint32_t*>(lds_c + kStreamR0 + (s & 127u) * 4u);
+      };
+      // byte offset of relative position p in this lane's chunk at rowa, clamped to [0, 16]
+      auto cpos = [&](uint32_t p, uint32_t rowa) -> uint32_t {
+        return p <= rowa ? 0u : min(p - rowa, 16u);
+      };
+      // the next block of the window becomes the current one (ends: group-uniform)
+      auto advance = [&](bool ends, uint32_t ns, uint32_t nw) {
+        if (ends) {
+          fl &= ~kOpen;
+          cur++;
+          wi++;
+          cs = ns;
+          ce = nw & 0x7fffffffu;
+          if (cur >= nb) fl |= kIdle | kOpen;  // the sub-piece's last block has ended
+        }
+      };
+
+      // One row of the lean path, w = this lane's 16 bytes of relative row rr.
+      // The caller has checked that no group ends two blocks in one row, and
+      // made room (slots, window) for every block end of its rows.
+      auto row = [&](u32x4 w, uint32_t rr) {
+        STEP_ROW(w);  // c = T(c) ^ w: every lane, the whole row inside its block
+        if (ev == rr) {  // (group-uniform) the row holds a block boundary of this group
+          const bool open = fl & kOpen;
+          // T(c), the braids advanced by the row before its bytes: c ^ w
+          uint32_t a0 = open ? c0 ^ w.x : 0u, a1 = open ? c1 ^ w.y : 0u;
+          uint32_t a2 = open ? c2 ^ w.z : 0u, a3 = open ? c3 ^ w.w : 0u;
+          const uint32_t rowa = rr * (uint32_t)kRowBytes + 16u * li;  // this lane's chunk (relative)
+          // A: the current block, open or starting here (a gap row has neither)
+          const bool startsA = !open && (cs >> 7) == rr;
+          const bool inA = open || startsA;
+          const uint32_t loA = startsA ? cpos(cs, rowa) : 0u;
+          part(w, loA, inA ? max(cpos(ce, rowa), loA) : loA, startsA, cs, a0, a1, a2, a3);
+          const bool endsA = inA && end_row(cs, ce) == rr;
+          // B: the next block, when A ends here (it starts here or later)
+          const uint32_t nsrc = g * 8u + ((wi + 1u) & 7u);
+          const uint32_t ns = (uint32_t)__shfl((int)ws, (int)nsrc);
+          const uint32_t nw = (uint32_t)__shfl((int)we, (int)nsrc);
+          const bool startsB = endsA && (ns >> 7) == rr && cur + 1u < nb;
+          uint32_t y0 = 0u, y1 = 0u, y2 = 0u, y3 = 0u;
+          const uint32_t loB = cpos(ns, rowa);
+          part(w, loB, startsB ? max(cpos(nw & 0x7fffffffu, rowa), loB) : loB, startsB, ns, y0, y1, y2, y3);
+          save(endsA, a0, a1, a2, a3);
+          c0 = endsA ? y0 : a0;
+          c1 = endsA ? y1 : a1;
+          c2 = endsA ? y2 : a2;
+          c3 = endsA ? y3 : a3;
+          if (inA) fl |= kOpen;
+          advance(endsA, ns, nw);
+          if (startsB) fl |= kOpen;
+          ev = next_ev(rr);
+        }
+      };
+
+      // The general row (a rolled loop runs it): any number of block ends,
+      // flushing the slots and refilling the window as they fill up.
+      auto row_general = [&](u32x4 w, uint32_t rr) {
+        STEP_ROW(w);
+        const bool slow = ev == rr;
+        const bool open0 = fl & kOpen;
+        uint32_t x0 = open0 ? c0 ^ w.x : 0u, x1 = open0 ? c1 ^ w.y : 0u;
+        uint32_t x2 = open0 ? c2 ^ w.z : 0u, x3 = open0 ? c3 ^ w.w : 0u;
+        const uint32_t rowa = rr * (uint32_t)kRowBytes + 16u * li;
+        bool act = slow;
+        while (__ballot(act) != 0ull) {
+          bool ends = false;
+          if (act) {
+            const bool open = fl & kOpen;
+            const bool starts = !open && (cs >> 7) == rr;
+            if (open || starts) {
+              const uint32_t lo = starts ? cpos(cs, rowa) : 0u;
+              part(w, lo, max(cpos(ce, rowa), lo), starts, cs, x0, x1, x2, x3);
+              fl |= kOpen;
+              ends = end_row(cs, ce) == rr;
+            }
+          }
+          act = ends;
+          if (__ballot(ends) != 0ull) {
+            if (__ballot(ends && cnt == kSlots) != 0ull) flush();
+            save(ends, x0, x1, x2, x3);
+            if (ends) x0 = x1 = x2 = x3 = 0u;
+            if (__ballot(ends && wi == 7u) != 0ull) {  // the window restarts at cur + 1
+              const uint32_t wb = ends && wi == 7u ? cur + 1u : cur - wi;
+              uint32_t nws = (uint32_t)__shfl((int)sr, (int)((wb + li) & 63u));
+              uint32_t nwe = (uint32_t)__shfl((int)er, (int)((wb + li) & 63u));
+              if (wb + li >= nb) nws = nwe = 0x7fffff00u;
+              if (ends && wi == 7u) {
+                ws = nws;
+                we = nwe;
+                wi = ~0u;  // (advance makes it 0)
+              }
+            }
+            const uint32_t nsrc = g * 8u + ((wi + 1u) & 7u);
+            const uint32_t ns = (uint32_t)__shfl((int)ws, (int)nsrc);
+            const uint32_t nw = (uint32_t)__shfl((int)we, (int)nsrc);
+            advance(ends, ns, nw);
+            if (fl & kIdle) act = false;
+          }
+        }
+        if (slow) {
+          c0 = x0;
+          c1 = x1;
+          c2 = x2;
+          c3 = x3;
+          ev = next_ev(rr);
+        }
+      };
+
+      // ---- the segment: half-steps of kBank rows, two banks in flight ----
+      const uint32_t voff = seg0 * (uint32_t)kRowBytes + 16u * li - (uint32_t)(desc - pb);  // (wraps: reads 0)
+      auto ld = [&](uint32_t r) -> u32x4 {
+        return __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + r * (uint32_t)kRowBytes, 0, kStreamAux));
+      };
+      u32x4 ba[kBank], bb[kBank];
+#pragma unroll
+      for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
+#pragma unroll
+      for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(kBank + k);
+      // Half-steps of kBank rows.  Before a half-step every group gets room for
+      // the block ends of its rows: the window restarts at its current block
+      // once it is half used, and the slots are flushed when they cannot take
+      // the ends.  This is done for the next half-step after a bank has been
+      // absorbed and before it is reloaded, so that only the other bank is live
+      // across the flush.  The lean rows then need no flush (at most kSlots
+      // ends per group, no two in one row); otherwise the general rows.
+      bool lean = true;
+      auto prepare = [&](uint32_t r) {  // for rows r .. r+kBank-1
+        const uint32_t rr0 = seg0 + r;
+        if (__ballot(wi >= 4u) != 0ull) {  // the window restarts at the current block
+          ws = (uint32_t)__shfl((int)sr, (int)((cur + li) & 63u));
+          we = (uint32_t)__shfl((int)er, (int)((cur + li) & 63u));
+          if (cur + li >= nb) ws = we = 0x7fffff00u;
+          wi = 0;
+        }
+        const uint32_t wre = end_row(ws, we & 0x7fffffffu);
+        const uint64_t mh = __ballot(li >= wi && wre < rr0 + kBank);
+        const uint32_t ne = (uint32_t)__builtin_popcount((uint32_t)(mh >> (8u * g)) & 0xffu);
+        if (__ballot(cnt + ne > kSlots) != 0ull) flush();
+        const uint32_t wre_next = (uint32_t)__shfl_down((int)wre, 1);
+        const bool twice = li >= wi && li + 1u < wi + ne && wre == wre_next;
+        lean = __ballot(ne > kSlots || twice) == 0ull;
+      };
+      auto half = [&](u32x4 (&X)[kBank], uint32_t r) {
+        const uint32_t rr0 = seg0 + r;
+        if (__builtin_expect(lean, 1)) {
+#pragma unroll
+          for (uint32_t k = 0; k < kBank; k++)
+            if (r + k < Q) row(X[k], rr0 + k);
+        } else {
+          // more block ends than slots, or two in one row (short blocks)
+#pragma unroll 1
+          for (uint32_t k = 0; k < kBank && r + k < Q; k++)
+            row_general(k == 0 ? X[0] : (k == 1 || kBank == 2) ? X[1] : X[kBank - 1], rr0 + k);
+        }
+      };
+      prepare(0);
+      for (uint32_t r = 0; r < Q; r += 2 * kBank) {
+        half(ba, r);
+        prepare(r + kBank);
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(r + 2 * kBank + k);
+        if (r + kBank < Q) half(bb, r + kBank);
+        prepare(r + 2 * kBank);
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(r + 3 * kBank + k);
+      }
+      flush();
+
+      // ---- blocks that cross segments ----
+      // T: the braids of the block still open at the segment end, shifted to
+      // that block's last row; summed per block over consecutive groups, and
+      // added to the block's head where it ends.
+      const bool tvalid = (fl & (kIdle | kOpen)) == kOpen;
+      uint32_t xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+      const uint32_t kt = tvalid ? end_row(cs, ce) - (seg0 + Q - 1u) : 0u;  // rows to its last row
+      const u32x4 scols = *reinterpret_cast<gptr_u32x4>(
+          reinterpret_cast<uint64_t>(&dc->shift_cols[kt & (kShiftCols - 1u)][4 * li]));
+      xt = cols_apply(scols, xt, li);
+      if (tvalid && kt >= kShiftCols) xt = shift_rows(g_lds, dc, xt, kt & ~(kShiftCols - 1u));
+      uint32_t v = tvalid ? xt : 0u;
+      const uint32_t key = tvalid ? cur : ~0u;
+#pragma unroll
+      for (uint32_t d = 8; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, d);
+        const uint32_t tk = (uint32_t)__shfl_up((int)key, d);
+        if (lane >= d && tk == key) v ^= t;
+      }
+      const uint32_t pv = (uint32_t)__shfl_up((int)v, 8);
+      const uint32_t pk = (uint32_t)__shfl_up((int)key, 8);
+      const bool hvalid = fl & kHValid;
+      const bool hadd = g > 0 && hvalid && pk == first;
+      finish(hvalid, hv ^ (hadd ? pv : 0u), first);
+      b0 += nb;
+    }
+    if (!chunked) break;
+    pi += (uint32_t)nwaves;
+    if (pi >= p_end) break;
+    b_lo = bnd[pi];
+    b_hi = bnd[pi + 1];
+  }
+  store_parked();
+  if (__ballot(huge) != 0ull) {
+    // The units walk redoes this wave's whole range (the same results for the
+    // blocks already done; their bad-block count is dropped, the walk counts).
+    units_fallback<kFallbackRows, kMode, kExt>(args, wave, nwaves, r_lo, r_hi, chunked, pi0, p_end);
+    return;
+  }
+  if (nbad && args.nbad) atomicAdd(args.nbad, nbad);
+}
+
+// Which batches go this way: no per-block init (crc32c::Value semantics;
+// init injection is a table lookup), and one of the modes below.
+bool stream_eligible(const RaggedArgs& a) {
+  if (a.init || a.n >= 0xffffff00ull) return false;  // (block indices are 32-bit in the kernel)
+  switch (a.mode) {
+    case kModeOut: return a.extents == kExtOffsets || a.extents == kExtHandles;
+    case kModeVerify: return a.extents == kExtOffsets;
+    case kModeSstCrc:
+    case kModeSstVerify: return a.extents == kExtHandles;
+    case kModeLogSeal:
+    case kModeLogVerify: return a.extents == kExtLogHeaders;
+    default: return false;
+  }
+}
+
+hipError_t launch_stream(const RaggedArgs& a, int grid, hipStream_t stream) {
+#define LSBM_LAUNCH_STREAM(R, M, X) \
+  hipLaunchKernelGGL((crc32c_stream_kernel<R, M, X>), dim3(grid), dim3(kStreamThreads), 0, stream, a)
+  switch (a.mode) {
+    case kModeOut:
+      if (a.extents == kExtOffsets) LSBM_LAUNCH_STREAM(32, kModeOut, kExtOffsets);
+      else LSBM_LAUNCH_STREAM(32, kModeOut, kExtHandles);
+      break;
+    case kModeVerify: LSBM_LAUNCH_STREAM(32, kModeVerify, kExtOffsets); break;
+    case kModeSstCrc: LSBM_LAUNCH_STREAM(32, kModeSstCrc, kExtHandles); break;
+    case kModeSstVerify: LSBM_LAUNCH_STREAM(32, kModeSstVerify, kExtHandles); break;
+    case kModeLogSeal: LSBM_LAUNCH_STREAM(16, kModeLogSeal, kExtLogHeaders); break;
+    case kModeLogVerify: LSBM_LAUNCH_STREAM(16, kModeLogVerify, kExtLogHeaders); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LSBM_LAUNCH_STREAM
+  return hipGetLastError();
+}
+
+}  // namespace lsbm

@@ -11,6 +11,10 @@ constexpr int kGroupLanes = 8;
 constexpr int kWaveLanes = 64;
 constexpr int kBlockThreads = 1024;
 constexpr int kWavesPerWg = kBlockThreads / kWaveLanes;
+// The stream kernel (crc32c_stream.hip): 12 waves per CU, 168 VGPRs each
+// (its state does not fit 128 without spilling in the row loop).
+constexpr int kStreamThreads = 768;
+constexpr int kStreamWavesPerWg = kStreamThreads / kWaveLanes;
 constexpr uint32_t kLdsByteTabBytes = 131072;
 // Nibble tables (byte offsets into LDS).  Bases are chosen so that an
 // and-or can merge the nibble field with the base (disjoint bits).
@@ -20,8 +24,17 @@ constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane sl
 constexpr uint32_t kRowPowTables = 21;
 constexpr uint32_t kNibRowPow = kNibFin + 8 * 16 * 32 * 4;  // A^(128 * 2^i), i = 0..20
 constexpr uint32_t kNibNeg4 = kNibRowPow + kRowPowTables * 512;  // A^-4 (init injection)
-constexpr uint32_t kLdsBytes = kNibNeg4 + 512;
+// Stream kernel (crc32c_stream.hip): byte masks of a lane's 16-B chunk and
+// the row-start init injections.
+constexpr uint32_t kStreamHM = kNibNeg4 + 512;  // KM[lo][hi], 0 <= lo <= hi <= 16: the bytes
+                                                // [lo, hi) of a 16-B chunk (4 words, 16-B
+                                                // aligned), entry lo * 17 - lo (lo - 1) / 2 + hi - lo
+constexpr uint32_t kStreamMasks = 17 * 18 / 2;
+constexpr uint32_t kStreamR0 = kStreamHM + kStreamMasks * 16;  // R0[d] = A^-d(~0), d = 0..127
+constexpr uint32_t kLdsBytes = kStreamR0 + 128 * 4;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
+static_assert(kLdsBytes % 16 == 0 && kLdsBytes <= 160u * 1024u, "one LDS image per CU");
+static_assert(kStreamHM % 16 == 0, "ds_read_b128 of a mask");
 
 constexpr uint32_t kShiftCols = 512;  // unit shifts up to 511 rows (64 KiB frames) by columns
 constexpr uint32_t kFinCols = 129;    // A^-z (z < 128) and A^(1 - z) (type-byte extension)
