@@ -193,6 +193,18 @@ int lsbm_fill_splitmix64_dev(void* d_buf, uint64_t nbytes, uint64_t seed, void* 
  * loads), into d_sink[0..1023]: the measured read ceiling for that pattern. */
 int lsbm_stream_read_dev(const void* d_buf, uint64_t nbytes, uint32_t* d_sink, void* stream);
 
+/* ---- testing ---- */
+/* Fault injection for the host layers' error-path tests: the next pipeline of
+ * SealTables / VerifyTables / the log layer returns IOError("injected fault")
+ * after enqueueing `chunks` chunks, as a failed copy or launch would (-1:
+ * disarm).  Not for production use. */
+int lsbm_test_fail_host_pipeline(int chunks);
+/* Ragged-batch kernel policy (what LSBM_RAGGED_KERNEL sets at start-up): 0 the
+ * default (the stream kernel for offsets[] batches, the units kernel for the
+ * rest), 1 the units kernel for every batch, 2 the stream kernel for every
+ * batch it takes.  Results are identical; for tests and A/B runs. */
+int lsbm_test_ragged_kernel(int which);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -51,6 +51,8 @@ SIGNATURES = {
     "lsbm_gather_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "lsbm_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),
     "lsbm_stream_read_dev": (_int, [_vp, _u64, _vp, _vp]),
+    "lsbm_test_fail_host_pipeline": (_int, [_int]),
+    "lsbm_test_ragged_kernel": (_int, [_int]),
     # include/lsbm_bloom.h
     "lsbm_bloom_hash": (_u32, [_vp, _sz, _u32]),
     "lsbm_bloom_filter_bytes": (_u64, [_u64, _int]),

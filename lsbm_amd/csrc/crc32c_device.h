@@ -25,7 +25,9 @@
 //   0x20000        nibble tables of A^4 (16 entries each: conflict-free)
 //   0x20800        nibble tables of A^(116-16li), replicated per lane slot
 //                  (lane & 31) like the byte tables: conflict-free.
-//   kNibRowPow     nibble tables of A^(128 * 2^i), i < 21 (ragged-path unit shifts)
+//   kNibRowPow     nibble tables of A^(128 * 2^i), 9 <= i < 21 (ragged-path unit
+//                  shifts of >= 512 rows); its first 9 slots: A^(2^i), i < 8,
+//                  and A^-128 (the stream kernel's per-lane finish)
 //   kNibNeg4       nibble tables of A^-4 (init injection)
 #pragma once
 #include <hip/hip_runtime.h>

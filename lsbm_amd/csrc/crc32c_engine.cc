@@ -32,6 +32,7 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uin
                         const DevConsts* dc, int grid, hipStream_t stream);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
 bool ragged_uses_stream(const RaggedArgs& a);
+int set_ragged_policy(int p);
 hipError_t launch_range_bounds(const RaggedArgs& a, uint64_t P, uint32_t* bounds, int grid,
                                hipStream_t stream);
 hipError_t launch_trailer_scatter(uint8_t* file, uint64_t limit, const uint64_t* handles, const uint8_t* types,
@@ -97,8 +98,11 @@ void build_consts(DevConsts* c) {
     const uint32_t q = w >> 9, nib = (w >> 5) & 15u, slot = w & 31u;
     c->lds_image[kNibFin / 4 + w] = c->fin_nib[slot & 7u][q * 16 + nib];
   }
-  for (uint32_t i = 0; i < kRowPowTables; i++)  // A^(128 * 2^i) = A^(2^(7+i))
+  for (uint32_t i = kRowPowLo; i < kRowPowTables; i++)  // A^(128 * 2^i) = A^(2^(7+i))
     memcpy(&c->lds_image[kNibRowPow / 4 + i * 128], c->pow_nib[7 + i], 512);
+  for (uint32_t i = 0; i < 8; i++)  // A^(2^i) (stream kernel finish)
+    memcpy(&c->lds_image[kNibPow2 / 4 + i * 128], c->pow_nib[i], 512);
+  gf2::nibble_tables(gf2::byte_pow(-128), &c->lds_image[kNibNeg128 / 4]);
   memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
   for (uint32_t lo = 0, t = 0; lo <= 16; lo++)  // stream kernel: bytes [lo, hi) of a 16-B chunk
     for (uint32_t hi = lo; hi <= 16; hi++, t++)
@@ -531,9 +535,13 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   // Small batches stay one pass: the second launch and the scratch cost a
   // fixed ~10 us, the two passes save ~0.13 us per block (config 1's 45K
   // blocks: 0.088 ms one pass, 0.099 ms two).
+  // Under hipGraph capture: one pass as well (no stream-ordered allocation
+  // inside a captured sequence; an unknown capture state counts as capturing).
   uint32_t* crcs = nullptr;
   static const bool one_pass = getenv("LSBM_SEAL_ONE_PASS") != nullptr;  // (A/B measurements)
-  if (one_pass || n_blocks < (1u << 17) ||
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+  if (one_pass || capturing || n_blocks < (1u << 17) ||
       hipMallocAsync(reinterpret_cast<void**>(&crcs), n_blocks * sizeof(uint32_t), s) != hipSuccess) {
     (void)hipGetLastError();
     a.file = d_file;
@@ -712,7 +720,7 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
   Staging& stg = g_staging[device];
   std::lock_guard<std::mutex> lock(stg.mu);
   const uint8_t* src = static_cast<const uint8_t*>(h_base);
-  const bool src_pinned = host_pinned(h_base);
+  const bool src_pinned = host_pinned(h_base, 1);  // (each chunk's range is checked before its DMA)
   // chunk size: LSBM_STAGE_CHUNK_MB overrides (tuning only; tools/host_sweep.py)
   static const uint64_t kChunkBytes = [] {
     const char* v = getenv("LSBM_STAGE_CHUNK_MB");
@@ -767,6 +775,7 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
     }
     s.h_off[cnt] = pos;
     if (h_init) memcpy(s.h_init, h_init + next, cnt * 4);
+    if (tight && pos) tight = host_pinned(src + h_offsets[next], pos);
     if (tight) {
       e = hipMemcpyAsync(s.d_data, src + h_offsets[next], pos, hipMemcpyHostToDevice, s.stream);
     } else {
@@ -858,6 +867,11 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host_multi(
   for (int d = 0; d < n_devices; d++)
     if (rc[d] != LSBM_OK) return fail(rc[d], err[d].c_str());
   return LSBM_OK;
+}
+
+// Testing (include/lsbm_crc32c.h): the ragged kernel policy.
+__attribute__((visibility("default"))) int lsbm_test_ragged_kernel(int which) {
+  return set_ragged_policy(which) == 0 ? LSBM_OK : fail(LSBM_ERR_INVALID, "policy 0, 1 or 2");
 }
 
 }  // extern "C"

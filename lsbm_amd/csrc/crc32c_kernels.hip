@@ -17,6 +17,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "crc32c_units.h"
 
 namespace lsbm {
@@ -366,12 +368,37 @@ hipError_t launch_stream(const RaggedArgs& a, int grid, hipStream_t stream);
 // and log headers with no per-block init stream their rows
 // (crc32c_stream_kernel; extents out of order just make shorter sub-pieces).
 // LSBM_RAGGED_KERNEL=units keeps every batch on the units kernel (A/B runs).
-bool ragged_uses_stream(const RaggedArgs& a) {
-  static const bool units_only = [] {
+// Which ragged kernel a batch runs on.  The stream kernel wins on offsets[]
+// batches of mixed block sizes (config 4: 80 vs 76 % of HBM peak) and loses
+// on SSTable and log images (blocks of ~4 KiB and less between trailers and
+// headers: 75-78 vs 80-82 %, 38-40 vs 44-48 %), so by
+// default only crc32c_batch / crc32c_verify batches take it.
+// LSBM_RAGGED_KERNEL=units | stream (or lsbm_test_ragged_kernel) overrides:
+// every batch on the units kernel, or every eligible one on the stream kernel.
+namespace {
+std::atomic<int> g_ragged_policy{-1};  // -1: not read yet; 0 default, 1 units, 2 stream
+int ragged_policy() {
+  int p = g_ragged_policy.load(std::memory_order_relaxed);
+  if (p < 0) {
     const char* v = getenv("LSBM_RAGGED_KERNEL");
-    return v && v[0] == 'u';
-  }();
-  return !units_only && stream_eligible(a);
+    p = v && v[0] == 'u' ? 1 : (v && v[0] == 's' ? 2 : 0);
+    int expect = -1;
+    if (!g_ragged_policy.compare_exchange_strong(expect, p)) p = expect;
+  }
+  return p;
+}
+}  // namespace
+
+bool ragged_uses_stream(const RaggedArgs& a) {
+  const int p = ragged_policy();
+  if (p == 1 || !stream_eligible(a)) return false;
+  return p == 2 || a.extents == kExtOffsets;
+}
+
+int set_ragged_policy(int p) {
+  if (p < 0 || p > 2) return -1;
+  g_ragged_policy.store(p);
+  return 0;
 }
 
 // grid: one workgroup per CU (the LDS image); the waves per workgroup differ

@@ -9,10 +9,12 @@
 // streamed regardless of block boundaries:
 //
 //   * a wave takes a piece of consecutive blocks (as the units kernel) and
-//     cuts it into sub-pieces of at most 256 blocks, whose extents it loads
-//     into registers (4 per lane) and checks: ascending and non-overlapping
-//     (s_j >= e_{j-1}), within a 2 GiB window.  A sub-piece that is not goes
-//     through the units walk instead (any order, any overlap);
+//     cuts it into sub-pieces of at most 64 blocks, whose extents it loads
+//     into registers (one per lane) and checks: ascending and non-overlapping
+//     (s_j >= e_{j-1}), within a 2 GiB window; a sub-piece ends before the
+//     first block that is not.  When that leaves fewer than 16 blocks (blocks
+//     out of order) or a block alone spans 2 GiB, the units walk (any order,
+//     any overlap) redoes the wave's range instead;
 //   * the sub-piece's rows [floor(s_first / 128), last row] are cut into 8
 //     segments of Q rows, one per lane group, and every group streams its
 //     segment row after row with the fixed kernel's access pattern: one 16-B
@@ -25,10 +27,16 @@
 //     the next block starts from zero braids with its init register ~0
 //     injected as A^-(s mod 128)(~0) at the row start (an LDS table), so that
 //     the register is exactly ~0 when its first byte is absorbed (:289);
-//   * every kR rows the slots are merged (merge_braids, lock-step over the
-//     groups) and finished: A^-z (z = the bytes after e in its last row), the
-//     mode (CRC, masked CRC, verify, SSTable trailer CRC / check, log header
-//     seal / check), results parked in lanes and written 8 per group at once;
+//   * when a group's two slots cannot take the block ends of the next rows,
+//     the slots are merged (merge_braids, lock-step over the groups) and each
+//     raw CRC goes to the lane of its block (block j of the sub-piece: lane j)
+//     by one ds_bpermute from the group where it ends;
+//   * at the sub-piece end every lane finishes its own block: A^-z (z = the
+//     bytes after e in its last row) from the LDS power tables, the mode
+//     (CRC, masked CRC, verify, SSTable trailer CRC / check, log header seal /
+//     check) against the stored value it loaded when the sub-piece began,
+//     and one coalesced store per wave (no global load or store in the row
+//     loop besides the rows);
 //   * a block that crosses into the next group's segment leaves its braids
 //     there at the segment end (T); the group where it ends saves the rest
 //     (its head).  At the sub-piece end T pieces are merged, shifted to the
@@ -44,6 +52,22 @@
 #include "crc32c_units.h"
 
 namespace lsbm {
+
+#ifdef LSBM_STREAM_STATS
+// diagnostic counters (tools/stream_stats.sh): wave-rows, slow wave-rows,
+// general half-steps, general iterations, flushes, slot merges, sub-pieces,
+// group events
+// and wave cycles in: sub-piece setup, row loop, flushes, general half-steps,
+// prepare, sub-piece tail
+__device__ unsigned long long g_stream_stats[16];
+#define LSBM_STAT(i, v) (st[i] += (v))
+#define LSBM_TIC(i) const uint64_t tic_##i = __builtin_readcyclecounter()
+#define LSBM_TOC(i) (tm[i] += __builtin_readcyclecounter() - tic_##i)
+#else
+#define LSBM_STAT(i, v) ((void)0)
+#define LSBM_TIC(i) ((void)0)
+#define LSBM_TOC(i) ((void)0)
+#endif
 
 constexpr uint32_t kSubBlocks = 64;   // blocks per sub-piece: one extent per lane
 constexpr uint32_t kSlots = 2;        // block ends saved per group between flushes
@@ -67,13 +91,23 @@ __device__ __forceinline__ uint32_t end_row(uint32_t s, uint32_t e) {
   return e > s ? (e - 1u) >> 7 : s >> 7;
 }
 
-// A block of 2 GiB or more: the units walk over the wave's range, out of
-// line (its registers are not the stream loop's).
+// A block of 2 GiB or more, or blocks out of order: the units walk over the
+// wave's range, out of line (its registers are not the stream loop's).
+// It takes nothing from the caller but the kernel's argument block (read
+// again from the kernarg segment) and recomputes the wave's range: a call
+// with arguments would make the kernel copy them to scratch at its entry,
+// every wave, whether or not it falls back (~13 MB of writes per launch).
 template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
-__device__ __attribute__((noinline)) void units_fallback(RaggedArgs args, uint64_t wave, uint64_t nwaves,
-                                                         uint64_t b0, uint64_t b1, bool chunked,
-                                                         uint32_t pi, uint32_t p_end) {
-  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b0, b1, chunked, pi, p_end, false);
+__device__ __attribute__((noinline)) void units_fallback(const RaggedArgs* __restrict__ ka) {
+  const RaggedArgs args = *ka;
+  const uint64_t wave = (uint64_t)blockIdx.x * kStreamWavesPerWg +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kStreamWavesPerWg;
+  bool chunked;
+  uint32_t pi, p_end;
+  uint64_t b_lo, b_hi;
+  wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
+  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, false);
 }
 
 template <uint32_t kR, uint32_t kMode, uint32_t kExt>
@@ -84,7 +118,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   constexpr bool kSstModes = kMode == kModeSstVerify || kMode == kModeSstCrc;
   constexpr uint32_t kFallbackRows = kSstModes ? kSstUnitRows : LSBM_UNIT_ROWS;
   // group state bits (fl)
-  constexpr uint32_t kOpen = 1u, kHeadSeg = 2u, kIdle = 4u, kHValid = 16u;
+  constexpr uint32_t kOpen = 1u, kIdle = 4u;
   const DevConsts* __restrict__ dc = args.dc;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
@@ -108,46 +142,38 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const char* lds_c = reinterpret_cast<const char*>(g_lds);
 
-  // ---- results: parked one per lane, written 8 per group at once ----
-  uint32_t pend_i = ~0u;  // this lane's parked block (~0 = none; n < 2^32 - 1)
-  uint64_t pend_h = 0;    // (log seal: its header)
-  uint32_t pend_v = 0;
-  uint32_t npark = 0;     // results parked in this group
-  uint32_t nbad = 0;      // (lane 0 of each group)
-  (void)pend_h;
-  auto store_parked = [&]() {
-    if (pend_i != ~0u) {
-      if constexpr (kMode == kModeLogSeal) {
-        if (args.file) {  // header[0..4): one unaligned dword store
-          typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
-          *reinterpret_cast<gu32u>(pend_h) = pend_v;
-        }
-        if (args.out) args.out[pend_i] = pend_v;
-      } else if constexpr (kMode == kModeOut || kMode == kModeSstCrc) {
-        args.out[pend_i] = pend_v;
-      } else {
-        args.ok[pend_i] = (uint8_t)pend_v;
-      }
-    }
-    pend_i = ~0u;
-    npark = 0;
-  };
+  uint32_t nbad = 0;  // bad blocks (wave-uniform)
 
-  const uint64_t r_lo = b_lo, r_hi = b_hi;  // (the range, for the fallback)
-  const uint32_t pi0 = pi;
-  bool huge = false;  // a block of >= 2 GiB: the units walk redoes this wave's range
+#ifdef LSBM_STREAM_STATS
+  uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  bool huge = false;  // a block of >= 2 GiB, or blocks out of order: the units walk redoes this wave's range
+  // The next sub-piece's extents are loaded while this one streams (its log
+  // record lengths, loads that depend on them, behind its first rows): a
+  // sub-piece starts without waiting for them.
+  ExtRaw nx = {0, 0};
+  uint64_t nx_b = ~0ull;  // nx holds the raw extents of blocks nx_b + lane
   for (;;) {  // pieces (one, or this wave's range of every chunk)
     for (uint64_t b0 = b_lo; b0 < b_hi;) {
       // ---- the next sub-piece: up to 64 blocks in order (s_j >= e_{j-1}) ----
+      LSBM_STAT(6, 1u);
+      LSBM_TIC(0);
       const uint32_t navail = b_hi - b0 < kSubBlocks ? (uint32_t)(b_hi - b0) : kSubBlocks;
       uint32_t sr, er;  // relative to pb; er carries bit 31 for a record that does not fit
       uint64_t pb, desc;
       uint32_t nrec, NR, nb;
+      uint32_t aux = 0;  // this lane's block's expected / stored CRC or type byte (loaded now, used at the end)
       {
         const bool vq = lane < navail;
         const uint64_t bj = vq ? b0 + lane : b0;
-        ExtRaw rq = load_ext_raw(args, bj);
-        if constexpr (kExt == kExtLogHeaders) log_length(args, rq);
+        ExtRaw rq;
+        if (nx_b == b0) {
+          rq = nx;
+        } else {
+          rq = load_ext_raw(args, bj);
+          if constexpr (kExt == kExtLogHeaders) log_length(args, rq);
+        }
         uint64_t sa, ea, at;
         bool fits;
         extent_from_raw(args, bj, rq, sa, ea, fits, at);
@@ -170,12 +196,30 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           b0 += 1;
           continue;
         }
+        if (nb < kSubBlocks / 4u && nb < navail) {
+          // Blocks out of order (e.g. log headers passed by length): a sub-piece
+          // of a few blocks costs its setup and tail per block; the units walk
+          // (any order) redoes this wave's range instead.
+          huge = true;
+          break;
+        }
         const uint64_t e_last = readlane64(ea, nb - 1u), s_last = readlane64(sa, nb - 1u);
         desc = pb + ((uint32_t)(s_first - pb) & ~15u);  // chunks in [desc, roundup16(e_last)) are read
         nrec = (uint32_t)(((e_last + 15u) & ~15ull) - desc);
         sr = lane < nb ? (uint32_t)(sa - pb) : 0x7fffff00u;
         er = lane < nb ? (uint32_t)(ea - pb) | (fits ? 0u : 0x80000000u) : 0x7fffff00u;
         NR = end_row((uint32_t)(s_last - pb), (uint32_t)(e_last - pb)) + 1u;
+        // the stored / written checksum: after the type byte, or in the log
+        // header (6 bytes before the record's CRC bytes)
+        const bool mine = lane < nb;
+        uint64_t q = dummy;
+        if constexpr (kMode == kModeVerify) q = mine ? reinterpret_cast<uint64_t>(args.expect + bj) : dummy;
+        if constexpr (kMode == kModeSstCrc) q = mine ? reinterpret_cast<uint64_t>(args.types + bj) : dummy;
+        if constexpr (kMode == kModeSstVerify) q = mine && fits ? ea : dummy;
+        if constexpr (kMode == kModeLogVerify) q = mine && fits ? sa - 6u : dummy;
+        if constexpr (kMode == kModeVerify) aux = *reinterpret_cast<gptr_u32>(q);
+        if constexpr (kMode == kModeSstCrc) aux = *reinterpret_cast<gptr_u8>(q);
+        if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify) aux = *reinterpret_cast<gptr_u32u>(q);
       }
       // (wave-uniform: readfirstlane keeps the descriptor in SGPRs, with no
       // waterfall loop around the loads)
@@ -185,20 +229,31 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       pb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pb) |
            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pb >> 32)) << 32);
       NR = (uint32_t)__builtin_amdgcn_readfirstlane((int)NR);
+      nx_b = b0 + nb;
+      if (nx_b < b_hi) {  // (clamped as above)
+        const uint64_t na = b_hi - nx_b < kSubBlocks ? b_hi - nx_b : kSubBlocks;
+        nx = load_ext_raw(args, lane < na ? nx_b + lane : nx_b);
+      } else {
+        nx_b = ~0ull;
+      }
       const __amdgpu_buffer_rsrc_t rsrc =
           __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(desc), (short)0, (int)nrec, 0x00020000);
       const uint32_t Q = (NR + 7u) >> 3;  // rows per segment
       const uint32_t seg0 = g * Q;        // this group's first row (relative to pb)
-      // the first block of this group's segment: the number of blocks that end before it
-      uint32_t cur = 0;
+      // the first block of this group's segment: the number of blocks that
+      // end before it; and the group where this lane's block ends (its lane 0:
+      // the block's raw CRC is delivered from there)
+      uint32_t cur = 0, fsrc = 0;
       {
         const uint32_t re = end_row(sr, er & 0x7fffffffu);
 #pragma unroll
         for (uint32_t gg = 1; gg < 8; gg++) {
           const uint32_t f = (uint32_t)__builtin_popcountll(__ballot(lane < nb && re < gg * Q));
           cur = g == gg ? f : cur;
+          fsrc += re >= gg * Q ? 32u : 0u;  // (bpermute address of lane 8 gg)
         }
       }
+      uint32_t px = 0;  // this lane's block's raw CRC at the end of its last row
 
       // ---- the group's window: lane li holds block (cur - wi) + li ----
       // (a block past the sub-piece never starts or ends)
@@ -211,8 +266,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       uint32_t ce = (uint32_t)__shfl((int)we, (int)(g * 8u)) & 0x7fffffffu;
       uint32_t fl = 0;
       if (cur >= nb) fl |= kIdle | kOpen;
-      else if ((cs >> 7) < seg0) fl |= kOpen | kHeadSeg;  // continued from the previous segment
-      const uint32_t first = cur;
+      else if ((cs >> 7) < seg0) fl |= kOpen;  // continued from the previous segment
       // the next row that needs the slow path: the current block's last row,
       // its first row, the next row (a gap: no block open), never (idle)
       auto next_ev = [&](uint32_t rr) -> uint32_t {
@@ -224,90 +278,24 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       uint32_t cnt = 0;
       uint32_t sx0[4] = {0, 0, 0, 0}, sx1[4] = {0, 0, 0, 0};
       uint32_t sb0 = 0, sb1 = 0;
-      uint32_t hv = 0;  // the raw CRC of the head block (block `first`, continued from the previous segment)
 
-      // Finish block b0 + j for this group (act: group-uniform); every lane
-      // executes it (cols_apply sums over the group; the extents come from the
-      // lane that loaded them).  X = the block's raw CRC at the end of its
-      // last row.
-      auto finish = [&](bool act, uint32_t X, uint32_t j) {
-        const uint32_t bs = (uint32_t)__shfl((int)sr, (int)(j & 63u));
-        const uint32_t bw = (uint32_t)__shfl((int)er, (int)(j & 63u));
-        const uint32_t be = bw & 0x7fffffffu;
-        const uint32_t bi = (uint32_t)b0 + j;
-        const bool bad = (bw >> 31) != 0u;
-        const bool empty = bs == be;
-        const uint32_t z = (0u - be) & 127u;  // bytes of the last row after e (pb is 128-aligned)
-        // A^-z, or A^(1-z) when the type byte follows (WriteRawBlock's Extend)
-        uint32_t fi = kMode == kModeSstCrc ? 128u - z : 127u - z;
-        fi = act ? fi : 127u;
-        const u32x4 cols =
-            *reinterpret_cast<gptr_u32x4>(reinterpret_cast<uint64_t>(&dc->fin_cols[fi][4 * li]));
-        // the stored / written checksum: after the type byte, or the log header
-        // (6 bytes before the record's CRC bytes: it may lie before pb)
-        const uint64_t at = kMode == kModeSstVerify ? pb + be : pb + bs - 6u;
-        uint64_t q = dummy;
-        if constexpr (kMode == kModeVerify) q = act ? reinterpret_cast<uint64_t>(args.expect + bi) : dummy;
-        if constexpr (kMode == kModeSstCrc) q = act ? reinterpret_cast<uint64_t>(args.types + bi) : dummy;
-        if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify) q = act && !bad ? at : dummy;
-        asm volatile("" : "+v"(q));
-        uint32_t aux = 0;
-        if constexpr (kMode == kModeVerify) aux = *reinterpret_cast<gptr_u32>(q);
-        if constexpr (kMode == kModeSstCrc) aux = *reinterpret_cast<gptr_u8>(q);
-        if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify)
-          aux = *reinterpret_cast<gptr_u32u>(q);
-        uint32_t l = cols_apply(cols, X, li);
-        // an empty block leaves the init register ~0 (advanced by the type byte's slot)
-        if (empty) l = kMode == kModeSstCrc ? advance_byte(0xffffffffu) : 0xffffffffu;
-        const uint32_t crc = l ^ 0xffffffffu;
-        uint32_t val;
-        bool put = act;
-        if constexpr (kMode == kModeOut) {
-          val = (args.flags & 1u) ? mask_crc(crc) : crc;
-        } else if constexpr (kMode == kModeVerify) {
-          const bool good = ((args.flags & 1u) ? mask_crc(crc) : crc) == aux;
-          if (act && !good && li == 0) nbad++;
-          val = good ? 1u : 0u;
-        } else if constexpr (kMode == kModeSstCrc) {  // table/table_builder.cc:245-249
-          if (act && bad && li == 0) nbad++;
-          val = bad ? 0u : mask_crc((l ^ advance_byte(aux & 0xffu)) ^ 0xffffffffu);
-        } else if constexpr (kMode == kModeLogSeal) {  // common/log_writer.cc:85-88
-          if (act && bad && li == 0) {
-            if (args.out) args.out[bi] = 0;
-            nbad++;
-          }
-          put = act && !bad;
-          val = mask_crc(crc);
-        } else {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
-          const bool good = !bad && unmask_crc(aux) == crc;
-          if (act && !good && li == 0) nbad++;
-          val = good ? 1u : 0u;
-        }
-        // park it in lane (npark mod 8) of the group
-        if (__ballot(put && npark == 8u) != 0ull) store_parked();
-        if (put && li == (npark & 7u)) {
-          pend_i = bi;
-          pend_v = val;
-          if constexpr (kMode == kModeLogSeal) pend_h = at;
-        }
-        npark += put ? 1u : 0u;
-      };
       auto flush = [&]() {  // every lane active: merge and finish the saved blocks
+        LSBM_TIC(2);
+        LSBM_STAT(4, 1u);
 #pragma unroll 1
         for (uint32_t j = 0; j < kSlots; j++) {
           if (__ballot(cnt > j) == 0ull) break;
+          LSBM_STAT(5, 1u);
           const uint32_t X = merge_braids(g_lds, j ? sx1[0] : sx0[0], j ? sx1[1] : sx0[1],
                                           j ? sx1[2] : sx0[2], j ? sx1[3] : sx0[3], lane_fin);
-          const uint32_t bj = j ? sb1 : sb0;
-          const bool v = cnt > j;
-          const bool hd = v && bj == first && (fl & kHeadSeg);  // the segment's continued block
-          if (hd) {
-            hv = X;
-            fl |= kHValid;
-          }
-          finish(v && !hd, X, bj);
+          // lane l takes the CRC of block l from the group where it ends
+          const uint32_t bj = cnt > j ? (j ? sb1 : sb0) : ~0u;
+          const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
+          const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
+          if (bd == lane) px = xd;
         }
         cnt = 0;
+        LSBM_TOC(2);
       };
       static_assert(kSlots == 2, "two slots");
       // Save braids x of the block cur, which ends in this row, into the
@@ -364,6 +352,9 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // made room (slots, window) for every block end of its rows.
       auto row = [&](u32x4 w, uint32_t rr) {
         STEP_ROW(w);  // c = T(c) ^ w: every lane, the whole row inside its block
+        LSBM_STAT(0, 1u);
+        LSBM_STAT(1, __ballot(ev == rr) != 0ull ? 1u : 0u);
+        LSBM_STAT(7, (uint32_t)__builtin_popcountll(__ballot(ev == rr && li == 0u)));
         if (ev == rr) {  // (group-uniform) the row holds a block boundary of this group
           const bool open = fl & kOpen;
           // T(c), the braids advanced by the row before its bytes: c ^ w
@@ -407,6 +398,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         const uint32_t rowa = rr * (uint32_t)kRowBytes + 16u * li;
         bool act = slow;
         while (__ballot(act) != 0ull) {
+          LSBM_STAT(3, 1u);
           bool ends = false;
           if (act) {
             const bool open = fl & kOpen;
@@ -470,7 +462,13 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // ends per group, no two in one row); otherwise the general rows.
       bool lean = true;
       auto prepare = [&](uint32_t r) {  // for rows r .. r+kBank-1
+        LSBM_TIC(4);
         const uint32_t rr0 = seg0 + r;
+        if (__ballot(ev < rr0 + kBank) == 0ull) {  // no block boundary in these rows
+          lean = true;
+          LSBM_TOC(4);
+          return;
+        }
         if (__ballot(wi >= 4u) != 0ull) {  // the window restarts at the current block
           ws = (uint32_t)__shfl((int)sr, (int)((cur + li) & 63u));
           we = (uint32_t)__shfl((int)er, (int)((cur + li) & 63u));
@@ -484,20 +482,34 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         const uint32_t wre_next = (uint32_t)__shfl_down((int)wre, 1);
         const bool twice = li >= wi && li + 1u < wi + ne && wre == wre_next;
         lean = __ballot(ne > kSlots || twice) == 0ull;
+        LSBM_TOC(4);
       };
       auto half = [&](u32x4 (&X)[kBank], uint32_t r) {
         const uint32_t rr0 = seg0 + r;
-        if (__builtin_expect(lean, 1)) {
-#pragma unroll
-          for (uint32_t k = 0; k < kBank; k++)
-            if (r + k < Q) row(X[k], rr0 + k);
-        } else {
+        // (the lean rows follow the general ones rather than being their
+        // alternative: one path through the loop, no register copies where
+        // two paths would join)
+        uint32_t kdone = 0;
+        if (__builtin_expect(!lean, 0)) {
           // more block ends than slots, or two in one row (short blocks)
+          LSBM_STAT(2, 1u);
+          LSBM_TIC(3);
 #pragma unroll 1
           for (uint32_t k = 0; k < kBank && r + k < Q; k++)
             row_general(k == 0 ? X[0] : (k == 1 || kBank == 2) ? X[1] : X[kBank - 1], rr0 + k);
+          kdone = kBank;
+          LSBM_TOC(3);
         }
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++)
+          if (k >= kdone && r + k < Q) row(X[k], rr0 + k);
       };
+      LSBM_TOC(0);
+      LSBM_TIC(1);
+      // (the next sub-piece's record lengths: their header offsets arrive with
+      // the first bank, and the loads queue behind the banks)
+      if constexpr (kExt == kExtLogHeaders)
+        if (nx_b != ~0ull) log_length(args, nx);
       prepare(0);
       for (uint32_t r = 0; r < Q; r += 2 * kBank) {
         half(ba, r);
@@ -509,17 +521,19 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
 #pragma unroll
         for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(r + 3 * kBank + k);
       }
-      flush();
-
+      LSBM_TOC(1);
+      LSBM_TIC(5);
       // ---- blocks that cross segments ----
       // T: the braids of the block still open at the segment end, shifted to
       // that block's last row; summed per block over consecutive groups, and
-      // added to the block's head where it ends.
+      // added to the block's CRC in the lane that finishes it.  (The column
+      // load first: the last flush hides its latency.)
       const bool tvalid = (fl & (kIdle | kOpen)) == kOpen;
-      uint32_t xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
       const uint32_t kt = tvalid ? end_row(cs, ce) - (seg0 + Q - 1u) : 0u;  // rows to its last row
       const u32x4 scols = *reinterpret_cast<gptr_u32x4>(
           reinterpret_cast<uint64_t>(&dc->shift_cols[kt & (kShiftCols - 1u)][4 * li]));
+      flush();
+      uint32_t xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
       xt = cols_apply(scols, xt, li);
       if (tvalid && kt >= kShiftCols) xt = shift_rows(g_lds, dc, xt, kt & ~(kShiftCols - 1u));
       uint32_t v = tvalid ? xt : 0u;
@@ -530,27 +544,79 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         const uint32_t tk = (uint32_t)__shfl_up((int)key, d);
         if (lane >= d && tk == key) v ^= t;
       }
-      const uint32_t pv = (uint32_t)__shfl_up((int)v, 8);
-      const uint32_t pk = (uint32_t)__shfl_up((int)key, 8);
-      const bool hvalid = fl & kHValid;
-      const bool hadd = g > 0 && hvalid && pk == first;
-      finish(hvalid, hv ^ (hadd ? pv : 0u), first);
+      {  // the pieces summed up to the group before the one where block `lane` ends
+        const uint32_t pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fsrc - 32u), (int)v);
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fsrc - 32u), (int)key);
+        if (fsrc != 0u && pk == lane) px ^= pv;
+      }
+
+      // ---- finish: lane l, block b0 + l ----
+      {
+        const bool mine = lane < nb;
+        const uint32_t be = er & 0x7fffffffu;
+        const bool bad = (er >> 31) != 0u;
+        const bool empty = sr == be;
+        const uint32_t z = (0u - be) & 127u;  // bytes of the last row after e (pb is 128-aligned)
+        // A^-z, or A^(1-z) when the type byte follows (WriteRawBlock's Extend),
+        // as A^-128 A^m, m = 128 - z (+1): the LDS power tables, bit by bit
+        const uint32_t m = (kMode == kModeSstCrc ? 129u : 128u) - z;
+        uint32_t l = nib_lds_at(g_lds, kNibNeg128, px);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+          const uint32_t t = nib_lds_at(g_lds, kNibPow2 + i * 512u, l);
+          l = ((m >> i) & 1u) ? t : l;
+        }
+        // an empty block leaves the init register ~0 (advanced by the type byte's slot)
+        if (empty) l = kMode == kModeSstCrc ? advance_byte(0xffffffffu) : 0xffffffffu;
+        const uint32_t crc = l ^ 0xffffffffu;
+        const uint64_t bi = b0 + lane;
+        if constexpr (kMode == kModeOut) {
+          if (mine) args.out[bi] = (args.flags & 1u) ? mask_crc(crc) : crc;
+        } else if constexpr (kMode == kModeVerify) {
+          const bool good = ((args.flags & 1u) ? mask_crc(crc) : crc) == aux;
+          nbad += (uint32_t)__builtin_popcountll(__ballot(mine && !good));
+          if (mine) args.ok[bi] = good ? 1u : 0u;
+        } else if constexpr (kMode == kModeSstCrc) {  // table/table_builder.cc:245-249
+          nbad += (uint32_t)__builtin_popcountll(__ballot(mine && bad));
+          if (mine) args.out[bi] = bad ? 0u : mask_crc((l ^ advance_byte(aux & 0xffu)) ^ 0xffffffffu);
+        } else if constexpr (kMode == kModeLogSeal) {  // common/log_writer.cc:85-88
+          nbad += (uint32_t)__builtin_popcountll(__ballot(mine && bad));
+          const uint32_t val = mask_crc(crc);
+          if (mine && !bad && args.file) {  // header[0..4): one unaligned dword store
+            typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
+            *reinterpret_cast<gu32u>(pb + sr - 6u) = val;
+          }
+          if (mine && args.out) args.out[bi] = bad ? 0u : val;
+        } else {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+          const bool good = !bad && unmask_crc(aux) == crc;
+          nbad += (uint32_t)__builtin_popcountll(__ballot(mine && !good));
+          if (mine) args.ok[bi] = good ? 1u : 0u;
+        }
+      }
+      LSBM_TOC(5);
       b0 += nb;
     }
-    if (!chunked) break;
+    if (!chunked || huge) break;
     pi += (uint32_t)nwaves;
     if (pi >= p_end) break;
     b_lo = bnd[pi];
     b_hi = bnd[pi + 1];
   }
-  store_parked();
+#ifdef LSBM_STREAM_STATS
+  if (lane == 0u)
+    for (int i = 0; i < 8; i++) {
+      atomicAdd(&g_stream_stats[i], (unsigned long long)st[i]);
+      atomicAdd(&g_stream_stats[8 + i], (unsigned long long)tm[i]);
+    }
+#endif
   if (__ballot(huge) != 0ull) {
     // The units walk redoes this wave's whole range (the same results for the
     // blocks already done; their bad-block count is dropped, the walk counts).
-    units_fallback<kFallbackRows, kMode, kExt>(args, wave, nwaves, r_lo, r_hi, chunked, pi0, p_end);
+    units_fallback<kFallbackRows, kMode, kExt>(
+        (const RaggedArgs*)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
     return;
   }
-  if (nbad && args.nbad) atomicAdd(args.nbad, nbad);
+  if (lane == 0u && nbad && args.nbad) atomicAdd(args.nbad, nbad);
 }
 
 // Which batches go this way: no per-block init (crc32c::Value semantics;
@@ -588,3 +654,13 @@ hipError_t launch_stream(const RaggedArgs& a, int grid, hipStream_t stream) {
 }
 
 }  // namespace lsbm
+
+#ifdef LSBM_STREAM_STATS
+// diagnostic builds only: read and clear the counters
+extern "C" __attribute__((visibility("default"))) int lsbm_stream_stats(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lsbm::g_stream_stats), sizeof(unsigned long long) * 16) != hipSuccess)
+    return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(lsbm::g_stream_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -22,7 +22,13 @@ constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
 constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
                                          // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
 constexpr uint32_t kRowPowTables = 21;
-constexpr uint32_t kNibRowPow = kNibFin + 8 * 16 * 32 * 4;  // A^(128 * 2^i), i = 0..20
+constexpr uint32_t kNibRowPow = kNibFin + 8 * 16 * 32 * 4;  // A^(128 * 2^i), i = 9..20 (slot i)
+// Row shifts of 512 rows and more use slots 9..20; slots 0..8 hold the stream
+// kernel's finishing tables: A^(2^i), i = 0..7, and A^-128 (A^e, -128 < e <= 1,
+// as A^-128 A^(e + 128), bit by bit).
+constexpr uint32_t kRowPowLo = 9;
+constexpr uint32_t kNibPow2 = kNibRowPow;              // A^(2^i), i = 0..7: slot i
+constexpr uint32_t kNibNeg128 = kNibRowPow + 8 * 512;  // A^-128: slot 8
 constexpr uint32_t kNibNeg4 = kNibRowPow + kRowPowTables * 512;  // A^-4 (init injection)
 // Stream kernel (crc32c_stream.hip): byte masks of a lane's 16-B chunk and
 // the row-start init injections.

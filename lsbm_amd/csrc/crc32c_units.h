@@ -193,10 +193,14 @@ __device__ __forceinline__ uint32_t nib_lds_at(const uint32_t* lds, uint32_t tab
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
-// A^(128 k)(v), k rows: LDS tables for bits 0..kRowPowTables-1 of k, global ones beyond.
+// A^(128 k)(v), k rows, k a multiple of 2^kRowPowLo (the column tables take
+// the low bits): LDS tables for bits kRowPowLo..kRowPowTables-1 of k, global
+// ones beyond.
 __device__ __forceinline__ uint32_t shift_rows(const uint32_t* lds, const DevConsts* dc,
                                                uint32_t v, uint64_t k) {
-  for (uint32_t i = 0; k; i++, k >>= 1)
+  static_assert(kShiftCols == 1u << kRowPowLo, "column shifts cover the low bits");
+  k >>= kRowPowLo;
+  for (uint32_t i = kRowPowLo; k; i++, k >>= 1)
     if (k & 1u)
       v = i < kRowPowTables ? nib_lds_at(lds, kNibRowPow + i * 512, v) : nib_glb(dc->pow_nib[7 + i], v);
   return v;

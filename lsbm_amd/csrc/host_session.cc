@@ -1,6 +1,8 @@
 // host_session.cc -- see host_session.h.
 #include "host_session.h"
 
+#include <atomic>
+
 #include <string.h>
 
 #include <algorithm>
@@ -18,17 +20,39 @@ Status hip_status(hipError_t e, const char* what) {
   return Status::IOError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-bool host_pinned(const void* p) {
+namespace {
+bool pinned_byte(const void* p) {
   hipPointerAttribute_t attr;
-  if (!p || hipPointerGetAttributes(&attr, p) != hipSuccess) {
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();  // clear the sticky "invalid value" for pageable memory
     return false;
   }
   return attr.type == hipMemoryTypeHost;
 }
+}  // namespace
+
+// [p, p + n) page-locked: its first and last bytes are, and the allocation
+// holding p (when the runtime reports one) spans the whole range, so that a
+// registered prefix of a larger buffer does not pass as pinned.
+bool host_pinned(const void* p, size_t n) {
+  if (!p || n == 0 || !pinned_byte(p)) return false;
+  const char* last = static_cast<const char*>(p) + (n - 1);
+  if (!pinned_byte(last)) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && base) {
+    const char* b = static_cast<const char*>(base);
+    return static_cast<const char*>(p) >= b && last < b + size;
+  }
+  (void)hipGetLastError();
+  return true;
+}
 
 // ---- worker pool: one job at a time, the caller works on it too ----
 namespace {
+
+// set on the pool's threads, and on a caller while it works on its own job
+thread_local bool t_in_pool = false;
 
 class WorkPool {
  public:
@@ -43,7 +67,9 @@ class WorkPool {
       gen_++;
     }
     cv_.notify_all();
+    t_in_pool = true;
     work();
+    t_in_pool = false;
     std::unique_lock<std::mutex> l(mu_);
     done_cv_.wait(l, [&] { return finished_ == pieces_; });
     fn_ = nullptr;
@@ -57,6 +83,7 @@ class WorkPool {
     const unsigned nt = std::min(15u, hw > 1 ? hw - 1 : 1u);
     for (unsigned t = 0; t < nt; t++)
       threads_.emplace_back([this] {
+        t_in_pool = true;
         uint64_t seen = 0;
         for (;;) {
           {
@@ -104,8 +131,8 @@ HostSession* g_sessions[kMaxDevices] = {};
 }  // namespace
 
 void parallel_for(size_t pieces, const std::function<void(size_t)>& fn) {
-  if (pieces == 1) {
-    fn(0);
+  if (pieces == 1 || (pieces > 1 && t_in_pool)) {  // (nested: inline, the pool runs one job at a time)
+    for (size_t k = 0; k < pieces; k++) fn(k);
     return;
   }
   if (pieces > 1) pool()->run(pieces, fn);
@@ -197,7 +224,7 @@ hipError_t HostSession::wait(Stage& s) {
 hipError_t HostSession::upload(void* d, const void* h, size_t n) {
   if (n == 0) return hipSuccess;
   Stage& s0 = stage_[0];
-  if (host_pinned(h)) {
+  if (host_pinned(h, n)) {
     hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s0.stream);
     return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
   }
@@ -229,7 +256,7 @@ hipError_t HostSession::download(void* h, const void* d, size_t n) {
   if (n == 0) return hipSuccess;
   Stage& s0 = stage_[0];
   // (everything the caller enqueued on stage 0's stream comes first)
-  if (host_pinned(h)) {
+  if (host_pinned(h, n)) {
     hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s0.stream);
     return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
   }
@@ -273,9 +300,30 @@ void HostSession::ShutdownAll() {
 }
 
 // ---- lease ----
+// Every exit path of a layer (an error between enqueueing a chunk and
+// collecting it included) ends here: the stages' work is waited for and their
+// results dropped, so that no later call collects a stale chunk (its tag would
+// index that call's plan) and no DMA from the caller's memory is still in
+// flight when the layer returns.
 SessionLease::~SessionLease() {
+  if (s_)
+    for (int i = 0; i < HostSession::kStages; i++) {
+      Stage& sg = s_->stage(i);
+      if (sg.stream) (void)hipStreamSynchronize(sg.stream);
+      sg.busy = false;
+    }
   if (lock_.owns_lock()) lock_.unlock();
   delete guard_;
+}
+
+namespace {
+std::atomic<int> g_fault_after{-1};
+}  // namespace
+
+bool host_fault_point(size_t enqueued) {
+  int n = g_fault_after.load();
+  if (n < 0 || enqueued < (size_t)n) return false;
+  return g_fault_after.compare_exchange_strong(n, -1);
 }
 
 Status SessionLease::Open(int device) {
@@ -303,3 +351,10 @@ Status SessionLease::Open(int device) {
 }
 
 }  // namespace lsbm
+
+// Testing only (include/lsbm_crc32c.h): the next host-layer pipeline fails
+// once it has enqueued `chunks` chunks (-1: off).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_fail_host_pipeline(int chunks) {
+  lsbm::g_fault_after.store(chunks < 0 ? -1 : chunks);
+  return 0;
+}

@@ -119,6 +119,7 @@ class HostSession {
 
 // The device's session, locked for this caller, with the device current for
 // the lease's lifetime (the caller's current device is restored after).
+// On release every stage is drained and marked idle, whatever the caller left.
 class SessionLease {
  public:
   SessionLease() = default;
@@ -136,15 +137,24 @@ class SessionLease {
   std::unique_lock<std::mutex> lock_;
 };
 
-// Is p inside page-locked host memory (hipHostMalloc'd or registered)?
-bool host_pinned(const void* p);
+// Is [p, p + n) inside page-locked host memory (hipHostMalloc'd or registered)?
+bool host_pinned(const void* p, size_t n);
 
 // fn(0) ... fn(pieces - 1) over the worker pool (15 threads and the caller),
-// one job at a time; returns when all have run.
+// one job at a time; returns when all have run.  A call from inside a pool
+// task runs its pieces inline on that thread (no deadlock, no extra
+// parallelism).  Concurrent callers (host layers on different devices) take
+// turns for the whole pool: each job is one staging copy or one header pass,
+// about a millisecond, so the turns interleave finely.
 void parallel_for(size_t pieces, const std::function<void(size_t)>& fn);
 
 // memcpy of n bytes, split over the worker pool when n >= 4 MiB.
 void parallel_copy(void* dst, const void* src, size_t n);
+
+// Fault injection for the error-path tests (lsbm_test_fail_host_pipeline):
+// true once, when a pipeline that has enqueued `enqueued` chunks reaches the
+// armed count.
+bool host_fault_point(size_t enqueued);
 
 // Status for a failed HIP call.
 Status hip_status(hipError_t e, const char* what);

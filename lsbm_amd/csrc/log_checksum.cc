@@ -48,7 +48,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     while (i < n && heads[i] / kLogChunk == w) i++, c.count++;
     chunks.push_back(c);
   }
-  const bool pinned = host_pinned(img);
+  const bool pinned = host_pinned(img + lo, hi - lo);
   SessionLease s;
   Status st = s.Open(device);
   if (!st.ok()) return st;
@@ -66,6 +66,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
       st = finish(sg);
       if (!st.ok()) return st;
     }
+    if (host_fault_point(k)) return Status::IOError("injected fault");  // (tests)
     const Chunk& c = chunks[k];
     const uint64_t bytes = c.hi - c.lo;
     hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);

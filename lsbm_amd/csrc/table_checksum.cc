@@ -124,7 +124,7 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
   std::vector<size_t> ok_base(count + 1, 0);
   for (size_t t = 0; t < count; t++) ok_base[t + 1] = ok_base[t] + tables[t].n;
   std::vector<uint8_t> pinned(count);
-  for (size_t t = 0; t < count; t++) pinned[t] = host_pinned(tables[t].file);
+  for (size_t t = 0; t < count; t++) pinned[t] = host_pinned(tables[t].file, tables[t].file_size);
 
   SessionLease s;
   Status st = s.Open(device);
@@ -165,6 +165,7 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
       st = finish(sg);
       if (!st.ok()) return st;
     }
+    if (host_fault_point(c)) return Status::IOError("injected fault");  // (tests)
     const Chunk& ch = plan.chunks[c];
     hipError_t e = sg.bulk.reserve(std::max<size_t>(HostSession::kChunkBytes, ch.bytes));
     if (e == hipSuccess) e = sg.meta.reserve(meta_bytes);

@@ -13,7 +13,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "lsbm/log_checksum.h"
 #include "lsbm/table_checksum.h"
+#include "lsbm_crc32c.h"
 #include "util/crc32c.h"
 
 static int fails = 0;
@@ -128,6 +130,101 @@ int main() {
   for (size_t i = 0; i < oks.size(); i++) nbad += !oks[i];
   EXPECT(nbad == 1 && oks[base9 + 4] == 0);
   if (reg) (void)hipHostUnregister(&files[7][0]);
+
+  // ---- error paths: a pipeline that fails with chunks in flight ----
+  // (lsbm_test_fail_host_pipeline: the failure a copy or launch error would
+  // give, after two chunks were enqueued).  The next call must neither collect
+  // the failed call's chunks nor write their results: it seals byte for byte
+  // what a clean run does, and verify / read report every record.
+  {
+    const size_t ft = 4;
+    std::vector<std::string> f0(ft);
+    std::vector<std::vector<lsbm::BlockHandle>> fh(ft);
+    std::vector<std::vector<uint8_t>> fy(ft);
+    for (size_t t = 0; t < ft; t++) {
+      std::vector<uint64_t> sz(2800);
+      for (auto& x : sz) x = 3000 + rng() % 3000;  // ~12 MiB per table: ~12 MiB chunks
+      uint64_t fs = 0;
+      fh[t] = lsbm::LayoutBlocks(sz, &fs);
+      f0[t].assign(fs, '\0');
+      for (auto& c : f0[t]) c = (char)(' ' + rng() % 95);
+      fy[t].resize(sz.size());
+      for (auto& y : fy[t]) y = rng() & 1;
+    }
+    auto images = [&](std::vector<std::string>& f) {
+      std::vector<lsbm::TableImage> v(ft);
+      for (size_t t = 0; t < ft; t++)
+        v[t] = lsbm::TableImage{&f[t][0], f[t].size(), fh[t].data(), fy[t].data(), fh[t].size()};
+      return v;
+    };
+    std::vector<std::string> fa = f0, fb = f0;
+    std::vector<lsbm::TableImage> ia = images(fa), ib = images(fb);
+    EXPECT(lsbm_test_fail_host_pipeline(2) == 0);
+    st = lsbm::SealTables(0, ia.data(), ft);
+    EXPECT(st.IsIOError() && st.ToString() == "IO error: injected fault");
+    st = lsbm::SealTables(0, ib.data(), ft);
+    EXPECT(st.ok());
+    size_t nchk = 0;
+    for (size_t t = 0; t < ft; t++) {
+      // only the trailers differ from the unsealed image, and each is the reference's
+      for (size_t i = 0; i < fh[t].size(); i++, nchk++) {
+        const char* block = fb[t].data() + fh[t][i].offset;
+        char trailer[5];
+        trailer[0] = (char)fy[t][i];
+        uint32_t crc = leveldb::crc32c::Extend(leveldb::crc32c::Value(block, fh[t][i].size), trailer, 1);
+        encode_fixed32(trailer + 1, leveldb::crc32c::Mask(crc));
+        EXPECT(memcmp(trailer, block + fh[t][i].size, 5) == 0);
+        memcpy(&f0[t][fh[t][i].offset + fh[t][i].size], trailer, 5);
+      }
+      EXPECT(f0[t] == fb[t]);
+    }
+    EXPECT(lsbm_test_fail_host_pipeline(1) == 0);
+    std::vector<uint8_t> okb;
+    st = lsbm::VerifyTables(0, ib.data(), ft, &okb);
+    EXPECT(st.IsIOError());
+    st = lsbm::VerifyTables(0, ib.data(), ft, &okb);
+    EXPECT(st.ok() && okb.size() == nchk);
+    for (uint8_t o : okb) EXPECT(o == 1);
+
+    // the log layer (log_checksum.cc): ~40 MiB of records, ~10 MiB chunks
+    lsbm::log::BatchWriter w;
+    std::vector<std::string> recs;
+    size_t total = 0;
+    while (total < (40u << 20)) {
+      std::string r(rng() % 5000, '\0');
+      for (auto& c : r) c = (char)(' ' + rng() % 95);
+      total += r.size();
+      w.AddRecord(r.data(), r.size());
+      recs.push_back(std::move(r));
+    }
+    EXPECT(lsbm_test_fail_host_pipeline(2) == 0);
+    st = w.Seal(0);
+    EXPECT(st.IsIOError());
+    st = w.Seal(0);  // the same headers again, from scratch
+    EXPECT(st.ok());
+    const std::string& img = w.contents();
+    size_t bad_headers = 0;
+    for (uint64_t hd : w.headers()) {
+      const uint8_t* hp = reinterpret_cast<const uint8_t*>(img.data() + hd);
+      const size_t len = hp[4] | (hp[5] << 8);
+      uint32_t stored;
+      memcpy(&stored, hp, 4);
+      bad_headers += leveldb::crc32c::Unmask(stored) != leveldb::crc32c::Value(img.data() + hd + 6, len + 1);
+    }
+    EXPECT(bad_headers == 0);
+    struct CountingReporter : lsbm::log::Reporter {
+      size_t n = 0;
+      void Corruption(size_t, const lsbm::Status&) override { n++; }
+    } rep;
+    std::vector<std::string> got;
+    std::vector<uint64_t> offs;
+    EXPECT(lsbm_test_fail_host_pipeline(1) == 0);
+    st = lsbm::log::ReadLog(0, img.data(), img.size(), &rep, &got, &offs);
+    EXPECT(st.IsIOError());
+    st = lsbm::log::ReadLog(0, img.data(), img.size(), &rep, &got, &offs);
+    EXPECT(st.ok() && rep.n == 0 && got == recs);
+    EXPECT(lsbm_test_fail_host_pipeline(-1) == 0);
+  }
   printf("%s (%zu blocks, %llu bytes; %zu blocks over %zu tables)\n", fails ? "FAILED" : "OK", n,
          (unsigned long long)file_size, checked, nt);
   return fails ? 1 : 0;

@@ -18,6 +18,16 @@ from golden.splitmix import stream_bytes
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _stream_for_every_mode(torch_cuda):
+    """Every batch the stream kernel takes goes to it here (by default only
+    offsets[] batches do: lsbm_amd/csrc/crc32c_kernels.hip ragged_uses_stream)."""
+    from lsbm_amd._lib import lib
+    assert lib().lsbm_test_ragged_kernel(2) == 0
+    yield
+    assert lib().lsbm_test_ragged_kernel(0) == 0
+
+
 def _dev(torch, arr, dtype=None):
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if dtype is not None:

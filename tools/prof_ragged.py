@@ -9,7 +9,8 @@ dispatch is profiled).
   sst       1M x 4,118-B blocks with trailers: lsbm_sst_verify_dev
   c4        2M blocks of config 4's Zipf lengths (23 GiB): lsbm_crc32c_batch_dev
 
-LSBM_RAGGED_KERNEL=units selects the units kernel (lsbm_amd/csrc/crc32c_kernels.hip).
+LSBM_RAGGED_KERNEL=units | stream selects the kernel (lsbm_amd/csrc/crc32c_kernels.hip
+ragged_uses_stream; by default offsets[] batches take the stream kernel).
 """
 import argparse
 import ctypes
@@ -29,6 +30,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("which")
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--stats", action="store_true",
+                   help="print the stream kernel's event counters (tools/stream_stats.sh build)")
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -89,9 +92,26 @@ def main():
         fn = lambda: engine.crc32c_batch(d, do, out=out, stream=s)
     else:
         raise SystemExit("unknown workload " + a.which)
+    if a.stats:
+        fn()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * 16)()
+        L.lsbm_stream_stats(buf)  # clear
     for _ in range(a.reps):
         fn()
     torch.cuda.synchronize()
+    if a.stats:
+        assert L.lsbm_stream_stats(buf) == 0
+        names = ["wave_rows", "slow_rows", "gen_halves", "gen_iters", "flushes", "merges",
+                 "subpieces", "group_events"]
+        st = {k: buf[i] / a.reps for i, k in enumerate(names)}
+        kib = d.numel() / 1024.0
+        print(a.which, " ".join(f"{k}={v:.0f}" for k, v in st.items()))
+        print(a.which, "per KiB:", " ".join(f"{k}={v / kib:.3f}" for k, v in st.items()))
+        tn = ["setup", "loop", "flush", "general", "prepare", "tail"]
+        tt = [buf[8 + i] / a.reps for i in range(len(tn))]
+        tot = tt[0] + tt[1] + tt[5]
+        print(a.which, "wave cycles %.3g:" % tot, " ".join(f"{k}={v / tot:.3f}" for k, v in zip(tn, tt)))
 
 
 if __name__ == "__main__":
