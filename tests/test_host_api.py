@@ -11,6 +11,8 @@ import os
 import re
 import subprocess
 
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -57,6 +59,48 @@ def test_scalar_api_matches_reference(product_lib, golden):
         blk = printable_bytes(b["seed"], b["len"]).tobytes()
         assert crc32c.extend(crc32c.value(blk), bytes([b["type"]])) == b["crc"]
     assert crc32c.MASK_DELTA == 0xA282EAD8
+
+
+def _aligned_copy(data, align):
+    """data at an address that is `align` mod 16 (the buffer stays alive with it)."""
+    buf = ctypes.create_string_buffer(len(data) + 64)
+    base = (ctypes.addressof(buf) + 15) & ~15
+    ctypes.memmove(base + align, data, len(data))
+    return buf, base + align
+
+
+def test_scalar_extend_at_golden_alignments(product_lib, golden):
+    """The golden cases at their recorded alignment (tests/golden/make_golden.py
+    placed each case's bytes `align` bytes past a 64-B boundary for the
+    reference's Extend; here past a 16-B one, the same mod 8 and 16): through
+    lsbm_crc32c_extend and through the C++ symbol
+    the unchanged table/ and log code links (its SSE4.2 path runs a byte-wise
+    prologue up to the first 8-B boundary, lsbm_amd/csrc/crc32c_host.cc)."""
+    L = product_lib
+    cxx = getattr(L, "_ZN7leveldb6crc32c6ExtendEjPKcm")
+    cxx.restype = ctypes.c_uint32
+    cxx.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    aligns = set()
+    for c in golden["random"]:
+        data = stream_bytes(c["seed"], 0, c["len"]).tobytes()
+        buf, p = _aligned_copy(data, c["align"])
+        aligns.add(c["align"])
+        assert L.lsbm_crc32c_extend(c["init"], ctypes.c_void_p(p), len(data)) == c["value"], c
+        assert cxx(c["init"], p, len(data)) == c["value"], c
+    assert len(aligns) >= 8  # the golden set spans the alignments
+
+
+def test_scalar_extend_every_alignment(product_lib, oracle):
+    """Every start alignment mod 16 and short / word-straddling lengths."""
+    L = product_lib
+    rng = np.random.default_rng(9)
+    for n in [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 33, 63, 65, 127, 255, 4096, 4101]:
+        data = stream_bytes(int(rng.integers(0, 2**62)), 0, n).tobytes()
+        init = int(rng.integers(0, 2**32))
+        want = oracle.extend(init, data)
+        for align in range(16):
+            buf, p = _aligned_copy(data, align)
+            assert L.lsbm_crc32c_extend(init, ctypes.c_void_p(p), n) == want, (n, align)
 
 
 def test_scalar_api_matches_oracle_sizes(product_lib, oracle):
