@@ -423,6 +423,23 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     assert r.stdout.startswith("OK")
 
 
+def test_level2_binding_over_the_reference_table_code(torch_cuda):
+    """integration/leveldb_gpu_checksum.h, linked with the reference's own
+    table/ and util/ objects (oracle/Makefile gpubind, built in the build
+    container): GPU-sealed trailers equal WriteRawBlock's, the reference's
+    ReadBlock accepts every block, and VerifyBlocksOnGpu fails a flipped byte
+    with ReadBlock's status.  Skipped where the binary was not built."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                       "gpu_binding")
+    if not os.access(exe, os.X_OK):
+        pytest.skip("oracle/_ref/gpu_binding not built (needs /root/reference at build time)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK"), r.stdout
+
+
 def test_cpp_block_compression_layer(torch_cuda, tmp_path):
     """include/lsbm/block_compression.h from C++: WriteBlock's compression and
     12.5% rule against the snappy oracle, ReadBlock's decompression and its
@@ -529,6 +546,69 @@ def test_ragged_batch_replays_in_a_hip_graph(torch_cuda, oracle):
         torch.cuda.synchronize()
         want = oracle.batch_offsets(stream_bytes(seed, 0, total + 16),
                                     offs.cpu().numpy().astype(np.uint64), masked=True)
+        assert np.array_equal(_u32(out), want)
+
+
+def test_two_pass_seal_and_chunked_batch_replay_in_a_hip_graph(torch_cuda, oracle):
+    """Under hipGraph capture the entry points that take stream-ordered scratch
+    when they run eagerly do without it: lsbm_sst_seal_dev at >= 131072 blocks
+    (two passes eagerly, the one-pass seal under capture) and a >= 4.2M-block
+    lsbm_crc32c_batch_dev (the chunked sweep's bounds eagerly, one range per
+    wave under capture).  Both captured, replayed over new bytes, checked
+    against the oracle (table/table_builder.cc:245-249, util/crc32c.cc:286-329)."""
+    torch = torch_cuda
+    from lsbm_amd import engine, table
+    rng = np.random.default_rng(0x6A)
+    # -- the seal: 140K blocks of 0..900 B
+    sizes = rng.integers(0, 900, size=140_000)
+    handles, total = table.layout_blocks(sizes)
+    dh = _dev(torch, handles.astype(np.int64))
+    types = rng.integers(0, 2, size=sizes.size).astype(np.uint8)
+    dt = _dev(torch, types)
+    img = torch.empty(total, dtype=torch.uint8, device="cuda")
+    nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        table.seal_blocks(img, dh, dt, stream=torch.cuda.current_stream(), nbad=nbad)
+    off, sz = handles[0::2], handles[1::2]
+    for seed in (0x6A0, 0x6A1):
+        engine.fill_splitmix64(img, seed)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        got = img.cpu().numpy()
+        src = stream_bytes(seed, 0, total)
+        # payloads untouched, every trailer the reference's
+        pick = np.concatenate([np.arange(64), rng.choice(sizes.size, 3000, replace=False),
+                               np.arange(sizes.size - 64, sizes.size)])
+        for i in pick:
+            o, n = int(off[i]), int(sz[i])
+            assert np.array_equal(got[o:o + n], src[o:o + n])
+            crc = oracle.mask(oracle.extend(oracle.value(src[o:o + n].tobytes()), bytes([types[i]])))
+            assert got[o + n] == types[i] and int.from_bytes(got[o + n + 1:o + n + 5].tobytes(), "little") == crc, i
+        ok, nb = table.verify_blocks(img, dh)
+        assert bool(ok.all().item()) and int(nb.item()) == 0 and int(nbad.item()) == 0
+    # -- the chunked sweep's batch size: 4.5M blocks of 0..120 B
+    n = 4_500_000
+    lens = rng.integers(0, 121, size=n)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    offs += 1
+    d = torch.empty(int(offs[-1]) + 16, dtype=torch.uint8, device="cuda")
+    do = _dev(torch, offs)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=s):
+        engine.crc32c_batch(d, do, out=out, stream=torch.cuda.current_stream())
+    for seed in (0x6B0, 0x6B1):
+        engine.fill_splitmix64(d, seed)
+        out.zero_()
+        g2.replay()
+        torch.cuda.synchronize()
+        want = oracle.batch_offsets(stream_bytes(seed, 0, d.numel()), offs.astype(np.uint64))
         assert np.array_equal(_u32(out), want)
 
 

@@ -43,3 +43,17 @@ def test_reference_table_and_log_link_unchanged(tmp_path):
                          os.path.join(REPO, "oracle", "_ref", "link_lsbm")],
                         capture_output=True, text=True).stdout
     assert "_ZN7leveldb6crc32c6ExtendEjPKcm" in nm and "_ZN7leveldb4HashEPKcmj" in nm
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "table")), reason="needs /root/reference")
+def test_level2_binding_compiles_and_links_against_the_reference():
+    """INTEGRATION.md's Level-2 binding is a real header
+    (integration/leveldb_gpu_checksum.h): compiled with the reference's own
+    flags and headers (leveldb::BlockHandle, Status, EncodeFixed32) and linked
+    with its table/ and util/ objects, the library and the HIP runtime
+    (oracle/Makefile gpubind).  tests/test_gpu_parity.py runs the binary."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "gpubind"], check=True)
+    exe = os.path.join(REPO, "oracle", "_ref", "gpu_binding")
+    assert os.access(exe, os.X_OK)
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "liblsbm_crc32c.so" in ldd and "libamdhip64" in ldd
