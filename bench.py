@@ -2,8 +2,10 @@
 """Headline benchmark: CRC32C GiB/s over device-resident 4 KiB SSTable blocks.
 
 Workload (BASELINE.json configs[1]): 1,048,576 blocks x
-4096 B = 4 GiB per GPU, stride 4096, bytes from the on-device splitmix64
-stream (seed 0x5EED0000 + rank), resident in HBM before timing starts.  One
+4096 B = 4 GiB per GPU, stride 4096, resident in HBM before timing starts.
+The bytes: one dataset, block i = bytes [4096 i, 4096 (i + 1)) of the
+splitmix64 stream 0x5EED0000 (tests/golden/splitmix.py), generated on the
+device; rank r of N holds global blocks [r n, (r + 1) n).  One
 *step* = one lsbm_crc32c_fixed_dev launch over the whole batch (crc32c::Value
 of every block, util/crc32c.cc:286-329).
 
@@ -14,8 +16,9 @@ WORLD_SIZE is unset, bench.py starts `python -m torch.distributed.run
 --nproc-per-node N ... bench.py` itself as a child process (before any GPU
 call) and exits with its return code; a WORLD_SIZE that differs from --gpus is
 an error.  Each rank checksums its own shard of 10M x 4 KiB blocks (BASELINE.json configs[4]:
-80M blocks over 8 GPUs; weak scaling, no data-path collective: blocks are
-independent).  --blocks overrides the per-GPU block count.  Timing: W untimed steps, barrier + synchronize, K
+the 80M-block dataset over 8 GPUs in contiguous ranges, blocks [10M r, 10M (r + 1)) on
+rank r, so any N checksums the same bytes for the same block; weak scaling, no
+data-path collective: blocks are independent).  --blocks overrides the per-GPU block count.  Timing: W untimed steps, barrier + synchronize, K
 steps between HIP events on the launch stream, barrier + synchronize, max over
 ranks.  Rank 0 prints ONE JSON line.
 
@@ -264,7 +267,9 @@ def main():
     engine.init(local)
     n = args.blocks or (NBLOCKS if world == 1 else NBLOCKS_MULTI)
     data = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-    engine.fill_splitmix64(data, SEED + rank)
+    # global blocks [lo, lo + n): the stream from byte 4096 lo, i.e. word 512 lo
+    lo = rank * n
+    engine.fill_splitmix64(data, SEED + lo * (BLOCK // 8))
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
 
@@ -319,7 +324,7 @@ def main():
     if args.dump_samples:  # tests/test_multirank_gpu.py checks these against the oracle
         idx = np.unique(np.concatenate([np.arange(min(n, 64)), np.arange(max(0, n - 64), n),
                                         np.random.default_rng(rank).integers(0, n, 128)]))
-        np.savez(f"{args.dump_samples}.rank{rank}.npz", idx=idx, seed=SEED + rank, n=n,
+        np.savez(f"{args.dump_samples}.rank{rank}.npz", gidx=lo + idx, seed=SEED, n=n,
                  crc=out.cpu().numpy().view(np.uint32)[idx], world=world, t_max=t_max)
 
     cpu = staged = None
@@ -341,7 +346,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic: on-device splitmix64 bytes (seed 0x{SEED:X} + rank), "
+            "data": f"synthetic: one dataset, block i = bytes [4096 i, 4096 (i+1)) of the splitmix64 "
+                    f"stream 0x{SEED:X}, generated on the device; rank r holds blocks [{n} r, {n} (r+1)); "
                     "resident in HBM before timing",
             "config": {"workload": workload, "blocks_per_gpu": n, "block_bytes": BLOCK,
                        "stride": BLOCK,

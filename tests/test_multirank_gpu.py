@@ -1,8 +1,9 @@
 """bench.py's N > 1 path on the one-GPU box: `python bench.py --gpus 2` starts
 its own two ranks (torch.distributed.run as a child process), each rank
-checksums its own config-5-shaped shard (10M x 4 KiB blocks, BASELINE.json
-configs[4]) on the HIP path, and the per-rank results are checked here against
-the oracle.  Both ranks share the one MI355X (LSBM_BENCH_DEVICES=1) and meet
+checksums its own config-5 shard on the HIP path: global blocks [10M r,
+10M (r + 1)) of the one 80M x 4 KiB dataset (BASELINE.json configs[4]; block i
+= bytes [4096 i, 4096 (i + 1)) of the splitmix64 stream 0x5EED0000), and the
+per-rank results are checked here against the oracle by global block index.  Both ranks share the one MI355X (LSBM_BENCH_DEVICES=1) and meet
 over gloo (LSBM_BENCH_BACKEND=gloo); the driver's 8-GPU run uses RCCL."""
 import glob
 import json
@@ -36,15 +37,19 @@ def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
     assert line["config"]["blocks_per_gpu"] == 10_000_000
     files = sorted(glob.glob(prefix + ".rank*.npz"))
     assert len(files) == 2
-    seeds = set()
+    seen = []
     for f in files:
         z = np.load(f)
         assert int(z["world"]) == 2 and int(z["n"]) == 10_000_000
-        seed = int(z["seed"])
-        seeds.add(seed)
-        for i, c in zip(z["idx"], z["crc"]):
-            assert c == oracle.value(stream_bytes(seed, int(i) * 4096, 4096).tobytes()), (f, int(i))
-    assert len(seeds) == 2  # each rank generated and checksummed its own shard
+        assert int(z["seed"]) == 0x5EED0000  # one dataset for every rank
+        rank = int(f.rsplit(".rank", 1)[1].split(".")[0])
+        g = z["gidx"].astype(np.int64)
+        assert g.min() >= rank * 10_000_000 and g.max() < (rank + 1) * 10_000_000
+        for i, c in zip(g, z["crc"]):
+            assert c == oracle.value(stream_bytes(0x5EED0000, int(i) * 4096, 4096).tobytes()), (f, int(i))
+        seen.append((g.min(), g.max()))
+    # rank 1's first block is global block 10M: the shards tile the dataset
+    assert sorted(seen)[1][0] == 10_000_000
 
 
 def test_bench_rejects_world_size_mismatch():
