@@ -104,10 +104,12 @@ void build_consts(DevConsts* c) {
     memcpy(&c->lds_image[kNibPow2 / 4 + i * 128], c->pow_nib[i], 512);
   gf2::nibble_tables(gf2::byte_pow(-128), &c->lds_image[kNibNeg128 / 4]);
   memcpy(&c->lds_image[kNibNeg4 / 4], c->neg4_nib, 512);
-  for (uint32_t lo = 0, t = 0; lo <= 16; lo++)  // stream kernel: bytes [lo, hi) of a 16-B chunk
-    for (uint32_t hi = lo; hi <= 16; hi++, t++)
+  for (uint32_t lo = 0; lo <= 16; lo++)  // stream kernel: bytes [lo, hi) of a 16-B chunk
+    for (uint32_t hi = lo; hi <= 16; hi++) {
+      const uint32_t t = km_entry(lo, hi);
       for (uint32_t b = 0; b < 16; b++)
         if (b >= lo && b < hi) c->lds_image[kStreamHM / 4 + t * 4 + b / 4] |= 0xffu << (8 * (b % 4));
+    }
   for (uint32_t d = 0; d < 128; d++)  // stream kernel: ~0 injected d bytes before the row start
     c->lds_image[kStreamR0 / 4 + d] = gf2::apply(gf2::byte_pow(-(int64_t)d), 0xffffffffu);
   memset(c->zero16, 0, sizeof(c->zero16));

@@ -369,10 +369,10 @@ hipError_t launch_stream(const RaggedArgs& a, int grid, hipStream_t stream);
 // (crc32c_stream_kernel; extents out of order just make shorter sub-pieces).
 // LSBM_RAGGED_KERNEL=units keeps every batch on the units kernel (A/B runs).
 // Which ragged kernel a batch runs on.  The stream kernel wins on offsets[]
-// batches of mixed block sizes (config 4: 80 vs 76 % of HBM peak) and loses
-// on SSTable and log images (blocks of ~4 KiB and less between trailers and
-// headers: 75-78 vs 80-82 %, 38-40 vs 44-48 %), so by
-// default only crc32c_batch / crc32c_verify batches take it.
+// batches of mixed block sizes (config 4: 78-80 vs 75-76 % of HBM peak) and
+// on log images (WAL records of 0-2,540 B: 45-53 vs 44-48 %) and loses on
+// SSTable images (4 KiB blocks between trailers: 74-77 vs 78-82 %; DESIGN.md
+// section 4), so by default offsets[] batches and log headers take it.
 // LSBM_RAGGED_KERNEL=units | stream (or lsbm_test_ragged_kernel) overrides:
 // every batch on the units kernel, or every eligible one on the stream kernel.
 namespace {
@@ -392,7 +392,7 @@ int ragged_policy() {
 bool ragged_uses_stream(const RaggedArgs& a) {
   const int p = ragged_policy();
   if (p == 1 || !stream_eligible(a)) return false;
-  return p == 2 || a.extents == kExtOffsets;
+  return p == 2 || a.extents == kExtOffsets || a.extents == kExtLogHeaders;
 }
 
 int set_ragged_policy(int p) {

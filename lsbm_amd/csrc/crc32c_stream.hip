@@ -69,8 +69,9 @@ __device__ unsigned long long g_stream_stats[16];
 #define LSBM_TOC(i) ((void)0)
 #endif
 
-constexpr uint32_t kSubBlocks = 64;   // blocks per sub-piece: one extent per lane
-constexpr uint32_t kSlots = 2;        // block ends saved per group between flushes
+constexpr uint32_t kSubBlocks = 63;   // blocks per sub-piece: one extent per lane; lane 63 always
+                                      // holds the sentinel block that never starts or ends
+constexpr uint32_t kSlots = 1;        // block ends saved per group between flushes
 constexpr int kStreamAux = 2;         // buffer-load policy: non-temporal (read once)
 constexpr uint32_t kBank = 3;         // rows per load bank (two in flight); round-2 A/B on the
                                       // fixed kernel: 3-6 rows per bank alike
@@ -117,8 +118,6 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   args.extents = kExt;
   constexpr bool kSstModes = kMode == kModeSstVerify || kMode == kModeSstCrc;
   constexpr uint32_t kFallbackRows = kSstModes ? kSstUnitRows : LSBM_UNIT_ROWS;
-  // group state bits (fl)
-  constexpr uint32_t kOpen = 1u, kIdle = 4u;
   const DevConsts* __restrict__ dc = args.dc;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
@@ -186,7 +185,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         // overlaps the one before; offsets that go back make an empty block
         // and then an earlier start) or that reaches 2 GiB past pb.
         const uint64_t pe = shfl_up64(ea, 1);
-        bool cut = !vq || ea - pb >= (1ull << 31) - 256u;
+        bool cut = !vq || ea - pb >= (1ull << 31) - 4096u;  // (rows stay below the sentinel's)
         if (lane > 0) cut = cut || sa < pe;
         const uint64_t cm = __ballot(cut);
         nb = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
@@ -255,41 +254,42 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       }
       uint32_t px = 0;  // this lane's block's raw CRC at the end of its last row
 
-      // ---- the group's window: lane li holds block (cur - wi) + li ----
-      // (a block past the sub-piece never starts or ends)
-      uint32_t wi = 0;
-      uint32_t ws = (uint32_t)__shfl((int)sr, (int)((cur + li) & 63u));
-      uint32_t we = (uint32_t)__shfl((int)er, (int)((cur + li) & 63u));
-      if (cur + li >= nb) ws = we = 0x7fffff00u;
-      // the current block [cs, ce) (relative to pb)
-      uint32_t cs = (uint32_t)__shfl((int)ws, (int)(g * 8u));
-      uint32_t ce = (uint32_t)__shfl((int)we, (int)(g * 8u)) & 0x7fffffffu;
-      uint32_t fl = 0;
-      if (cur >= nb) fl |= kIdle | kOpen;
-      else if ((cs >> 7) < seg0) fl |= kOpen;  // continued from the previous segment
-      // the next row that needs the slow path: the current block's last row,
-      // its first row, the next row (a gap: no block open), never (idle)
-      auto next_ev = [&](uint32_t rr) -> uint32_t {
-        return (fl & kIdle) ? ~0u : ((fl & kOpen) ? end_row(cs, ce) : min(cs >> 7, rr + 1u));
+      // ---- the group's two pointers into the sub-piece's blocks ----
+      // ep: the next block to end, sp: the next block to start (sp == ep + 1
+      // while block ep is open).  E = the end of block ep, S = the start of
+      // block sp with bit 31 set for a *short* block (one that starts and
+      // ends in the same row; an empty block is short and its end is taken
+      // as s + 1, so that it ends in its start row; its CRC does not use the
+      // braids).  Lane j holds block j's values; lanes >= nb sentinels that
+      // never start or end.  All group-uniform.
+      constexpr uint32_t kShort = 0x80000000u;
+      const uint32_t erm = er & 0x7fffffffu;
+      const uint32_t ej = erm == sr ? sr + 1u : erm;
+      const uint32_t sxl = sr | ((sr >> 7) == end_row(sr, erm) ? kShort : 0u);
+      auto pick = [&](uint32_t v, uint32_t j) -> uint32_t {  // block j's value (every lane active;
+        // j > 63: lane 63's sentinel)
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(j, 63u) << 2), (int)v);
       };
-      uint32_t ev = next_ev(seg0 - 1u);
+      uint32_t ep = cur, sp;
+      {
+        const uint32_t cs0 = pick(sr, ep);
+        sp = ep < nb && (cs0 >> 7) < seg0 ? ep + 1u : ep;  // continued from the previous segment
+      }
+      uint32_t E = pick(ej, ep), S = pick(sxl, sp);
       uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
       // saved block ends: braids and block (relative to b0)
       uint32_t cnt = 0;
-      uint32_t sx0[4] = {0, 0, 0, 0}, sx1[4] = {0, 0, 0, 0};
-      uint32_t sb0 = 0, sb1 = 0;
+      uint32_t sx0[4] = {0, 0, 0, 0};
+      uint32_t sb0 = 0;
 
       auto flush = [&]() {  // every lane active: merge and finish the saved blocks
         LSBM_TIC(2);
         LSBM_STAT(4, 1u);
-#pragma unroll 1
-        for (uint32_t j = 0; j < kSlots; j++) {
-          if (__ballot(cnt > j) == 0ull) break;
+        if (__ballot(cnt != 0u) != 0ull) {
           LSBM_STAT(5, 1u);
-          const uint32_t X = merge_braids(g_lds, j ? sx1[0] : sx0[0], j ? sx1[1] : sx0[1],
-                                          j ? sx1[2] : sx0[2], j ? sx1[3] : sx0[3], lane_fin);
+          const uint32_t X = merge_braids(g_lds, sx0[0], sx0[1], sx0[2], sx0[3], lane_fin);
           // lane l takes the CRC of block l from the group where it ends
-          const uint32_t bj = cnt > j ? (j ? sb1 : sb0) : ~0u;
+          const uint32_t bj = cnt != 0u ? sb0 : ~0u;
           const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
           const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
           if (bd == lane) px = xd;
@@ -297,149 +297,108 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         cnt = 0;
         LSBM_TOC(2);
       };
-      static_assert(kSlots == 2, "two slots");
-      // Save braids x of the block cur, which ends in this row, into the
-      // group's next slot (ends: group-uniform; the caller made room).
-      auto save = [&](bool ends, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
-        if (ends && cnt == 0u) {
-          sx0[0] = x0;
-          sx0[1] = x1;
-          sx0[2] = x2;
-          sx0[3] = x3;
-          sb0 = cur;
-        }
-        if (ends && cnt == 1u) {
-          sx1[0] = x0;
-          sx1[1] = x1;
-          sx1[2] = x2;
-          sx1[3] = x3;
-          sb1 = cur;
-        }
-        cnt += ends ? 1u : 0u;
+      static_assert(kSlots == 1, "one slot");
+      // Save braids x of block b, which ends in this row, into the group's
+      // slot (ends: group-uniform; the caller made room).
+      auto save = [&](bool ends, uint32_t b, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+        sx0[0] = ends ? x0 : sx0[0];
+        sx0[1] = ends ? x1 : sx0[1];
+        sx0[2] = ends ? x2 : sx0[2];
+        sx0[3] = ends ? x3 : sx0[3];
+        sb0 = ends ? b : sb0;
+        cnt = ends ? 1u : cnt;
       };
-      // The bytes [lo, hi) of this lane's chunk (0 <= lo <= hi <= 16), and the
-      // init register of a block that starts in this row at s (inject): the
-      // block's contribution to the row's braids.
-      auto part = [&](u32x4 w, uint32_t lo, uint32_t hi, bool inject, uint32_t s, uint32_t& x0,
-                      uint32_t& x1, uint32_t& x2, uint32_t& x3) {
-        const uint32_t t = lo * 17u - ((lo * (lo - 1u)) >> 1) + hi - lo;  // (lo = 0: hi)
-        const u32x4 m = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + t * 16u);
-        x0 ^= w.x & m.x;
-        x1 ^= w.y & m.y;
-        x2 ^= w.z & m.z;
-        x3 ^= w.w & m.w;
-        if (inject && li == 0u)  // the init register, d = s mod 128 bytes before s
-          x0 ^= *reinterpret_cast<const uint32_t*>(lds_c + kStreamR0 + (s & 127u) * 4u);
+      auto km = [&](uint32_t lo, uint32_t hi) -> u32x4 {  // bytes [lo, hi) of a chunk
+        return *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + km_entry(lo, hi) * 16u);
       };
-      // byte offset of relative position p in this lane's chunk at rowa, clamped to [0, 16]
-      auto cpos = [&](uint32_t p, uint32_t rowa) -> uint32_t {
-        return p <= rowa ? 0u : min(p - rowa, 16u);
-      };
-      // the next block of the window becomes the current one (ends: group-uniform)
-      auto advance = [&](bool ends, uint32_t ns, uint32_t nw) {
-        if (ends) {
-          fl &= ~kOpen;
-          cur++;
-          wi++;
-          cs = ns;
-          ce = nw & 0x7fffffffu;
-          if (cur >= nb) fl |= kIdle | kOpen;  // the sub-piece's last block has ended
-        }
+      auto clamp16 = [](uint32_t p, uint32_t rowa) -> uint32_t {  // p's offset in the chunk at rowa, in [0, 16]
+        return (uint32_t)min(max((int32_t)p - (int32_t)rowa, 0), 16);
       };
 
-      // One row of the lean path, w = this lane's 16 bytes of relative row rr.
-      // The caller has checked that no group ends two blocks in one row, and
-      // made room (slots, window) for every block end of its rows.
-      auto row = [&](u32x4 w, uint32_t rr) {
-        STEP_ROW(w);  // c = T(c) ^ w: every lane, the whole row inside its block
-        LSBM_STAT(0, 1u);
-        LSBM_STAT(1, __ballot(ev == rr) != 0ull ? 1u : 0u);
-        LSBM_STAT(7, (uint32_t)__builtin_popcountll(__ballot(ev == rr && li == 0u)));
-        if (ev == rr) {  // (group-uniform) the row holds a block boundary of this group
-          const bool open = fl & kOpen;
-          // T(c), the braids advanced by the row before its bytes: c ^ w
-          uint32_t a0 = open ? c0 ^ w.x : 0u, a1 = open ? c1 ^ w.y : 0u;
-          uint32_t a2 = open ? c2 ^ w.z : 0u, a3 = open ? c3 ^ w.w : 0u;
-          const uint32_t rowa = rr * (uint32_t)kRowBytes + 16u * li;  // this lane's chunk (relative)
-          // A: the current block, open or starting here (a gap row has neither)
-          const bool startsA = !open && (cs >> 7) == rr;
-          const bool inA = open || startsA;
-          const uint32_t loA = startsA ? cpos(cs, rowa) : 0u;
-          part(w, loA, inA ? max(cpos(ce, rowa), loA) : loA, startsA, cs, a0, a1, a2, a3);
-          const bool endsA = inA && end_row(cs, ce) == rr;
-          // B: the next block, when A ends here (it starts here or later)
-          const uint32_t nsrc = g * 8u + ((wi + 1u) & 7u);
-          const uint32_t ns = (uint32_t)__shfl((int)ws, (int)nsrc);
-          const uint32_t nw = (uint32_t)__shfl((int)we, (int)nsrc);
-          const bool startsB = endsA && (ns >> 7) == rr && cur + 1u < nb;
-          uint32_t y0 = 0u, y1 = 0u, y2 = 0u, y3 = 0u;
-          const uint32_t loB = cpos(ns, rowa);
-          part(w, loB, startsB ? max(cpos(nw & 0x7fffffffu, rowa), loB) : loB, startsB, ns, y0, y1, y2, y3);
-          save(endsA, a0, a1, a2, a3);
-          c0 = endsA ? y0 : a0;
-          c1 = endsA ? y1 : a1;
-          c2 = endsA ? y2 : a2;
-          c3 = endsA ? y3 : a3;
-          if (inA) fl |= kOpen;
-          advance(endsA, ns, nw);
-          if (startsB) fl |= kOpen;
-          ev = next_ev(rr);
-        }
+      // Every row is the row step; a row where some group starts or ends a
+      // block (nev, the group's next such row) is then fixed up.  A lean
+      // fix-up handles at most one end (block ep, open) and one start (block
+      // sp, not short) per group, as selects, with the LDS values it needs
+      // read when the previous event was handled (hidden behind the rows in
+      // between): mE = the bytes at or past E of this lane's chunk in row nev,
+      // mS = those at or past S, iv = block sp's init register ~0 as injected
+      // at its row start (A^-(S mod 128)(~0), util/crc32c.cc:289; lanes 1-7 of
+      // a group read a zero word, the empty mask), En / Sn = the pointers'
+      // next values.
+      uint32_t nev;
+      u32x4 mE, mS;
+      uint32_t iv, En, Sn;
+      auto next_event = [&]() {
+        nev = min(sp != ep ? (E - 1u) >> 7 : ~0u, (S & ~kShort) >> 7);
+        const uint32_t rowa = nev * (uint32_t)kRowBytes + 16u * li;
+        mE = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + clamp16(E, rowa) * 16u);
+        mS = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + clamp16(S & ~kShort, rowa) * 16u);
+        iv = *reinterpret_cast<const uint32_t*>(
+            lds_c + (li == 0u ? kStreamR0 + (S & 127u) * 4u : kStreamHM + km_entry(16u, 16u) * 16u));
+        En = pick(ej, ep + 1u);
+        Sn = pick(sxl, sp + 1u);
+      };
+      auto fix_lean = [&](u32x4 w, uint32_t rr) {  // after STEP_ROW: c = T(c) ^ w
+        const bool e_in = sp != ep && ((E - 1u) >> 7) == rr;
+        const bool s_in = ((S & ~kShort) >> 7) == rr;
+        if (__ballot(e_in && cnt == kSlots) != 0ull) flush();
+        LSBM_STAT(1, 1u);
+        // block ep through E: T(c) ^ (w & bytes < E) = c ^ (w & mE)
+        save(e_in, ep, __builtin_amdgcn_bitop3_b32(c0, w.x, mE.x, 0x78),
+             __builtin_amdgcn_bitop3_b32(c1, w.y, mE.y, 0x78), __builtin_amdgcn_bitop3_b32(c2, w.z, mE.z, 0x78),
+             __builtin_amdgcn_bitop3_b32(c3, w.w, mE.w, 0x78));
+        // block sp from S: its bytes of the row and its init register
+        c0 = s_in ? (w.x & mS.x) ^ iv : c0;
+        c1 = s_in ? w.y & mS.y : c1;
+        c2 = s_in ? w.z & mS.z : c2;
+        c3 = s_in ? w.w & mS.w : c3;
+        ep += e_in ? 1u : 0u;
+        E = e_in ? En : E;
+        sp += s_in ? 1u : 0u;
+        S = s_in ? Sn : S;
+        next_event();
       };
 
-      // The general row (a rolled loop runs it): any number of block ends,
-      // flushing the slots and refilling the window as they fill up.
-      auto row_general = [&](u32x4 w, uint32_t rr) {
-        STEP_ROW(w);
-        const bool slow = ev == rr;
-        const bool open0 = fl & kOpen;
-        uint32_t x0 = open0 ? c0 ^ w.x : 0u, x1 = open0 ? c1 ^ w.y : 0u;
-        uint32_t x2 = open0 ? c2 ^ w.z : 0u, x3 = open0 ? c3 ^ w.w : 0u;
+      // The general fix-up (a rolled loop runs it): any number of block ends
+      // and starts, in order, flushing the slot as it fills up.
+      auto fix_general = [&](u32x4 w, uint32_t rr) {  // after STEP_ROW
+        LSBM_STAT(2, 1u);
         const uint32_t rowa = rr * (uint32_t)kRowBytes + 16u * li;
-        bool act = slow;
-        while (__ballot(act) != 0ull) {
+        // the open block: its braids through the row start and its bytes of
+        // this row from lo on
+        const bool open0 = sp != ep;
+        uint32_t a0 = open0 ? c0 ^ w.x : 0u, a1 = open0 ? c1 ^ w.y : 0u;
+        uint32_t a2 = open0 ? c2 ^ w.z : 0u, a3 = open0 ? c3 ^ w.w : 0u;
+        uint32_t lo = 0;
+        for (;;) {
+          const bool open = sp != ep;
+          const bool ev_end = open && ((E - 1u) >> 7) == rr;
+          const bool ev_start = !open && ((S & ~kShort) >> 7) == rr;
+          if (__ballot(ev_end || ev_start) == 0ull) break;
           LSBM_STAT(3, 1u);
-          bool ends = false;
-          if (act) {
-            const bool open = fl & kOpen;
-            const bool starts = !open && (cs >> 7) == rr;
-            if (open || starts) {
-              const uint32_t lo = starts ? cpos(cs, rowa) : 0u;
-              part(w, lo, max(cpos(ce, rowa), lo), starts, cs, x0, x1, x2, x3);
-              fl |= kOpen;
-              ends = end_row(cs, ce) == rr;
-            }
+          if (__ballot(ev_end && cnt == kSlots) != 0ull) flush();
+          const u32x4 m = km(lo, max(clamp16(E, rowa), lo));
+          save(ev_end, ep, a0 ^ (w.x & m.x), a1 ^ (w.y & m.y), a2 ^ (w.z & m.z), a3 ^ (w.w & m.w));
+          const uint32_t inj = *reinterpret_cast<const uint32_t*>(lds_c + kStreamR0 + (S & 127u) * 4u);
+          if (ev_start) {
+            a0 = li == 0u ? inj : 0u;
+            a1 = a2 = a3 = 0u;
+            lo = clamp16(S & ~kShort, rowa);
           }
-          act = ends;
-          if (__ballot(ends) != 0ull) {
-            if (__ballot(ends && cnt == kSlots) != 0ull) flush();
-            save(ends, x0, x1, x2, x3);
-            if (ends) x0 = x1 = x2 = x3 = 0u;
-            if (__ballot(ends && wi == 7u) != 0ull) {  // the window restarts at cur + 1
-              const uint32_t wb = ends && wi == 7u ? cur + 1u : cur - wi;
-              uint32_t nws = (uint32_t)__shfl((int)sr, (int)((wb + li) & 63u));
-              uint32_t nwe = (uint32_t)__shfl((int)er, (int)((wb + li) & 63u));
-              if (wb + li >= nb) nws = nwe = 0x7fffff00u;
-              if (ends && wi == 7u) {
-                ws = nws;
-                we = nwe;
-                wi = ~0u;  // (advance makes it 0)
-              }
-            }
-            const uint32_t nsrc = g * 8u + ((wi + 1u) & 7u);
-            const uint32_t ns = (uint32_t)__shfl((int)ws, (int)nsrc);
-            const uint32_t nw = (uint32_t)__shfl((int)we, (int)nsrc);
-            advance(ends, ns, nw);
-            if (fl & kIdle) act = false;
-          }
+          ep += ev_end ? 1u : 0u;
+          sp += ev_start ? 1u : 0u;
+          const uint32_t nE = pick(ej, ep), nS = pick(sxl, sp);
+          E = ev_end ? nE : E;
+          S = ev_start ? nS : S;
         }
-        if (slow) {
-          c0 = x0;
-          c1 = x1;
-          c2 = x2;
-          c3 = x3;
-          ev = next_ev(rr);
+        if (sp != ep) {  // the block still open continues with its bytes [lo, 16) of the row
+          const u32x4 m = km(lo, 16u);
+          c0 = a0 ^ (w.x & m.x);
+          c1 = a1 ^ (w.y & m.y);
+          c2 = a2 ^ (w.z & m.z);
+          c3 = a3 ^ (w.w & m.w);
         }
+        next_event();
       };
 
       // ---- the segment: half-steps of kBank rows, two banks in flight ----
@@ -453,56 +412,35 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
 #pragma unroll
       for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(kBank + k);
-      // Half-steps of kBank rows.  Before a half-step every group gets room for
-      // the block ends of its rows: the window restarts at its current block
-      // once it is half used, and the slots are flushed when they cannot take
-      // the ends.  This is done for the next half-step after a bank has been
-      // absorbed and before it is reloaded, so that only the other bank is live
-      // across the flush.  The lean rows then need no flush (at most kSlots
-      // ends per group, no two in one row); otherwise the general rows.
-      bool lean = true;
-      auto prepare = [&](uint32_t r) {  // for rows r .. r+kBank-1
-        LSBM_TIC(4);
-        const uint32_t rr0 = seg0 + r;
-        if (__ballot(ev < rr0 + kBank) == 0ull) {  // no block boundary in these rows
-          lean = true;
-          LSBM_TOC(4);
-          return;
-        }
-        if (__ballot(wi >= 4u) != 0ull) {  // the window restarts at the current block
-          ws = (uint32_t)__shfl((int)sr, (int)((cur + li) & 63u));
-          we = (uint32_t)__shfl((int)er, (int)((cur + li) & 63u));
-          if (cur + li >= nb) ws = we = 0x7fffff00u;
-          wi = 0;
-        }
-        const uint32_t wre = end_row(ws, we & 0x7fffffffu);
-        const uint64_t mh = __ballot(li >= wi && wre < rr0 + kBank);
-        const uint32_t ne = (uint32_t)__builtin_popcount((uint32_t)(mh >> (8u * g)) & 0xffu);
-        if (__ballot(cnt + ne > kSlots) != 0ull) flush();
-        const uint32_t wre_next = (uint32_t)__shfl_down((int)wre, 1);
-        const bool twice = li >= wi && li + 1u < wi + ne && wre == wre_next;
-        lean = __ballot(ne > kSlots || twice) == 0ull;
-        LSBM_TOC(4);
-      };
+      next_event();
+      // Rows are fixed up lean until one where some group's next block to
+      // start is short; from there the rest of the bank goes through the
+      // general fix-up (one rolled copy of it).
       auto half = [&](u32x4 (&X)[kBank], uint32_t r) {
         const uint32_t rr0 = seg0 + r;
-        // (the lean rows follow the general ones rather than being their
-        // alternative: one path through the loop, no register copies where
-        // two paths would join)
-        uint32_t kdone = 0;
-        if (__builtin_expect(!lean, 0)) {
-          // more block ends than slots, or two in one row (short blocks)
-          LSBM_STAT(2, 1u);
+        uint32_t k0 = kBank;  // (wave-uniform)
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++) {
+          if (k0 == kBank && r + k < Q) {
+            STEP_ROW(X[k]);
+            LSBM_STAT(0, 1u);
+            if (__ballot(nev == rr0 + k) != 0ull) {
+              const bool gen = ((S & ~kShort) >> 7) == rr0 + k && (S & kShort) != 0u;
+              if (__builtin_expect(__ballot(gen) != 0ull, 0)) k0 = k;
+              else fix_lean(X[k], rr0 + k);
+            }
+          }
+        }
+        if (k0 < kBank) {
           LSBM_TIC(3);
 #pragma unroll 1
-          for (uint32_t k = 0; k < kBank && r + k < Q; k++)
-            row_general(k == 0 ? X[0] : (k == 1 || kBank == 2) ? X[1] : X[kBank - 1], rr0 + k);
-          kdone = kBank;
+          for (uint32_t k = k0; k < kBank && r + k < Q; k++) {
+            const u32x4 w = k == 0 ? X[0] : (k == 1 || kBank == 2) ? X[1] : X[kBank - 1];
+            if (k > k0) STEP_ROW(w);  // (row k0 has been stepped)
+            fix_general(w, rr0 + k);
+          }
           LSBM_TOC(3);
         }
-#pragma unroll
-        for (uint32_t k = 0; k < kBank; k++)
-          if (k >= kdone && r + k < Q) row(X[k], rr0 + k);
       };
       LSBM_TOC(0);
       LSBM_TIC(1);
@@ -510,14 +448,11 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // the first bank, and the loads queue behind the banks)
       if constexpr (kExt == kExtLogHeaders)
         if (nx_b != ~0ull) log_length(args, nx);
-      prepare(0);
       for (uint32_t r = 0; r < Q; r += 2 * kBank) {
         half(ba, r);
-        prepare(r + kBank);
 #pragma unroll
         for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(r + 2 * kBank + k);
         if (r + kBank < Q) half(bb, r + kBank);
-        prepare(r + 2 * kBank);
 #pragma unroll
         for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(r + 3 * kBank + k);
       }
@@ -528,8 +463,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // that block's last row; summed per block over consecutive groups, and
       // added to the block's CRC in the lane that finishes it.  (The column
       // load first: the last flush hides its latency.)
-      const bool tvalid = (fl & (kIdle | kOpen)) == kOpen;
-      const uint32_t kt = tvalid ? end_row(cs, ce) - (seg0 + Q - 1u) : 0u;  // rows to its last row
+      const bool tvalid = sp != ep && ep < nb;
+      const uint32_t kt = tvalid ? ((E - 1u) >> 7) - (seg0 + Q - 1u) : 0u;  // rows to its last row
       const u32x4 scols = *reinterpret_cast<gptr_u32x4>(
           reinterpret_cast<uint64_t>(&dc->shift_cols[kt & (kShiftCols - 1u)][4 * li]));
       flush();
@@ -537,7 +472,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       xt = cols_apply(scols, xt, li);
       if (tvalid && kt >= kShiftCols) xt = shift_rows(g_lds, dc, xt, kt & ~(kShiftCols - 1u));
       uint32_t v = tvalid ? xt : 0u;
-      const uint32_t key = tvalid ? cur : ~0u;
+      const uint32_t key = tvalid ? ep : ~0u;
 #pragma unroll
       for (uint32_t d = 8; d < 64; d <<= 1) {
         const uint32_t t = (uint32_t)__shfl_up((int)v, d);
@@ -549,7 +484,6 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fsrc - 32u), (int)key);
         if (fsrc != 0u && pk == lane) px ^= pv;
       }
-
       // ---- finish: lane l, block b0 + l ----
       {
         const bool mine = lane < nb;

@@ -11,9 +11,9 @@ constexpr int kGroupLanes = 8;
 constexpr int kWaveLanes = 64;
 constexpr int kBlockThreads = 1024;
 constexpr int kWavesPerWg = kBlockThreads / kWaveLanes;
-// The stream kernel (crc32c_stream.hip): 12 waves per CU, 168 VGPRs each
-// (its state does not fit 128 without spilling in the row loop).
-constexpr int kStreamThreads = 768;
+// The stream kernel (crc32c_stream.hip): 16 waves per CU, 128 VGPRs each
+// (A/B, round 3: 16 waves over 12 gain 4-8 points on WAL records).
+constexpr int kStreamThreads = 1024;
 constexpr int kStreamWavesPerWg = kStreamThreads / kWaveLanes;
 constexpr uint32_t kLdsByteTabBytes = 131072;
 // Nibble tables (byte offsets into LDS).  Bases are chosen so that an
@@ -34,8 +34,13 @@ constexpr uint32_t kNibNeg4 = kNibRowPow + kRowPowTables * 512;  // A^-4 (init i
 // the row-start init injections.
 constexpr uint32_t kStreamHM = kNibNeg4 + 512;  // KM[lo][hi], 0 <= lo <= hi <= 16: the bytes
                                                 // [lo, hi) of a 16-B chunk (4 words, 16-B
-                                                // aligned), entry lo * 17 - lo (lo - 1) / 2 + hi - lo
+                                                // aligned), entry km_entry(lo, hi)
 constexpr uint32_t kStreamMasks = 17 * 18 / 2;
+// Entry of KM[lo][hi]: the 17 masks [lo, 16) first (the lean rows' only
+// lookups, indexed by lo alone), then [lo, hi) for hi < 16 by lo, hi.
+constexpr uint32_t km_entry(uint32_t lo, uint32_t hi) {
+  return hi >= 16u ? lo : 17u + 16u * lo - ((lo * (lo - 1u)) >> 1) + hi - lo;
+}
 constexpr uint32_t kStreamR0 = kStreamHM + kStreamMasks * 16;  // R0[d] = A^-d(~0), d = 0..127
 constexpr uint32_t kLdsBytes = kStreamR0 + 128 * 4;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;

@@ -2,7 +2,10 @@
 #include "host_session.h"
 
 #include <atomic>
+#include <chrono>
 
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -154,11 +157,12 @@ void parallel_copy(void* dst, const void* src, size_t n) {
 
 // ---- buffers ----
 hipError_t StagePair::reserve(size_t bytes) {
-  if (bytes <= cap) return hipSuccess;
+  if (bytes <= cap && !mapped) return hipSuccess;
   release();
   bytes = std::max<size_t>(bytes, 1u << 16);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), bytes);
+  mapped = false;
   if (e != hipSuccess) {
     release();
     return e;
@@ -167,11 +171,29 @@ hipError_t StagePair::reserve(size_t bytes) {
   return hipSuccess;
 }
 
+hipError_t StagePair::reserve_mapped(size_t bytes) {
+  if (bytes <= cap && mapped) return hipSuccess;
+  release();
+  bytes = std::max<size_t>(bytes, 1u << 16);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), bytes,
+                               hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
+  if (e != hipSuccess) {
+    if (h) (void)hipHostFree(h);
+    h = d = nullptr;
+    return e;
+  }
+  mapped = true;
+  cap = bytes;
+  return hipSuccess;
+}
+
 void StagePair::release() {
   if (h) (void)hipHostFree(h);
-  if (d) (void)hipFree(d);
+  if (d && !mapped) (void)hipFree(d);
   h = d = nullptr;
   cap = 0;
+  mapped = false;
 }
 
 // ---- session ----
@@ -318,7 +340,24 @@ SessionLease::~SessionLease() {
 
 namespace {
 std::atomic<int> g_fault_after{-1};
+bool timing_on() {
+  static const bool on = [] {
+    const char* v = getenv("LSBM_HOST_TIMING");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 }  // namespace
+
+double HostTiming::now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+HostTiming::HostTiming(const char* w) : what(w), on(timing_on()), t0(on ? now() : 0.0) {}
+HostTiming::~HostTiming() {
+  if (on)
+    fprintf(stderr, "{\"host_timing\": \"%s\", \"total_ms\": %.3f, \"copy_ms\": %.3f, \"wait_ms\": %.3f, \"post_ms\": %.3f}\n",
+            what, (now() - t0) * 1e3, t[kCopy] * 1e3, t[kWait] * 1e3, t[kPost] * 1e3);
+}
 
 bool host_fault_point(size_t enqueued) {
   int n = g_fault_after.load();

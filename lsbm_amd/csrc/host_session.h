@@ -50,12 +50,19 @@ class DeviceGuard {
   hipError_t err_;
 };
 
-// A pinned host buffer and a device buffer of the same capacity.
+// A pinned host buffer and a device buffer of the same capacity.  A *mapped*
+// pair (reserve_mapped) is one coherent page-locked host buffer that `d`
+// addresses from the device: a kernel's results land in host memory with no
+// copy.  The layers take their per-block results this way: a device-to-host
+// copy queued behind the next chunk's bulk host-to-device copy finished
+// ~0.6 ms after its kernel and held the stage (profiles/r03/host_trace).
 struct StagePair {
   uint8_t* h = nullptr;
   uint8_t* d = nullptr;
   size_t cap = 0;
+  bool mapped = false;
   hipError_t reserve(size_t bytes);  // grows (never shrinks); contents are not kept
+  hipError_t reserve_mapped(size_t bytes);
   void release();
 };
 
@@ -150,6 +157,21 @@ void parallel_for(size_t pieces, const std::function<void(size_t)>& fn);
 
 // memcpy of n bytes, split over the worker pool when n >= 4 MiB.
 void parallel_copy(void* dst, const void* src, size_t n);
+
+// Diagnostics (LSBM_HOST_TIMING=1 in the environment): a layer's pipeline
+// adds the wall time of its phases and prints one line to stderr per call:
+// the host copy into pinned staging, waits for a stage, the host-side result
+// handling, and the whole call.
+struct HostTiming {
+  enum Phase { kCopy, kWait, kPost, kPhases };
+  explicit HostTiming(const char* what);
+  ~HostTiming();
+  void add(Phase p, double s) { t[p] += s; }
+  static double now();
+  const char* what;
+  bool on;
+  double t0, t[kPhases] = {0, 0, 0};
+};
 
 // Fault injection for the error-path tests (lsbm_test_fail_host_pipeline):
 // true once, when a pipeline that has enqueued `enqueued` chunks reaches the

@@ -35,6 +35,7 @@ namespace {
 Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint64_t* heads,
                size_t n, bool seal, uint8_t* res) {
   if (n == 0) return Status::OK();
+  HostTiming tm(seal ? "log_seal_device" : "log_verify_device");
   struct Chunk {
     uint64_t lo, hi;
     size_t first, count;
@@ -54,10 +55,13 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
   if (!st.ok()) return st;
   const size_t per = seal ? 4 : 1;
   auto finish = [&](Stage& sg) -> Status {
+    double t = tm.on ? HostTiming::now() : 0.0;
     const hipError_t e = s->wait(sg);
+    if (tm.on) tm.add(HostTiming::kWait, HostTiming::now() - t), t = HostTiming::now();
     if (e != hipSuccess) return hip_status(e, seal ? "seal" : "verify");
     const Chunk& c = chunks[sg.tag];
     memcpy(res + c.first * per, sg.res.h, c.count * per);
+    if (tm.on) tm.add(HostTiming::kPost, HostTiming::now() - t);
     return Status::OK();
   };
   for (size_t k = 0; k < chunks.size(); k++) {
@@ -71,14 +75,16 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     const uint64_t bytes = c.hi - c.lo;
     hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
     if (e == hipSuccess) e = sg.meta.reserve(c.count * sizeof(uint64_t));
-    if (e == hipSuccess) e = sg.res.reserve(c.count * per);
+    if (e == hipSuccess) e = sg.res.reserve_mapped(c.count * per);  // (the kernel writes the host buffer)
     if (e != hipSuccess) return hip_status(e, "staging buffers");
     uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
     for (size_t i = 0; i < c.count; i++) hh[i] = heads[c.first + i] - c.lo;
     if (pinned) {
       e = hipMemcpyAsync(sg.bulk.d, img + c.lo, bytes, hipMemcpyHostToDevice, sg.stream);
     } else {
+      const double t = tm.on ? HostTiming::now() : 0.0;
       parallel_copy(sg.bulk.h, img + c.lo, bytes);
+      if (tm.on) tm.add(HostTiming::kCopy, HostTiming::now() - t);
       e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, bytes, hipMemcpyHostToDevice, sg.stream);
     }
     if (e == hipSuccess)
@@ -91,9 +97,8 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
                         : lsbm_log_verify_dev(sg.bulk.d, bytes, d_h, c.count, sg.res.d, nullptr,
                                               sg.stream);
     if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
-    e = hipMemcpyAsync(sg.res.h, sg.res.d, c.count * per, hipMemcpyDeviceToHost, sg.stream);
-    if (e == hipSuccess) e = hipEventRecord(sg.done, sg.stream);
-    if (e != hipSuccess) return hip_status(e, "D2H");
+    e = hipEventRecord(sg.done, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "event");
     sg.busy = true;
     sg.tag = k;
   }
@@ -339,6 +344,7 @@ void BatchWriter::AddRecord(const char* data, size_t n) {
 Status BatchWriter::Seal(int device) {
   const size_t count = headers_.size() - sealed_;
   if (count == 0) return Status::OK();
+  HostTiming tm("BatchWriter::Seal");
   // the unsealed tail of the log: every pending header's masked crc (4 B each
   // come back), EncodeFixed32 into its header (util/coding.cc)
   std::unique_ptr<uint32_t[]> masked(new uint32_t[count]);

@@ -152,6 +152,35 @@ def test_stream_overlapping_and_unsorted_extents(torch_cuda, oracle):
     assert np.array_equal(got, want)
 
 
+def test_stream_gapped_extents(torch_cuda, oracle):
+    """Ordered extents with gaps of 0-400 bytes between them (a block's start
+    row after the row where the one before ends: no block open in between),
+    blocks ending on row ends, and short and empty blocks after gaps."""
+    from lsbm_amd import engine
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    n = 40_000
+    lens = rng.integers(0, 3000, size=n)
+    short = rng.random(n) < 0.1
+    lens[short] = rng.integers(0, 130, size=int(short.sum()))
+    gaps = rng.integers(0, 401, size=n)
+    gaps[rng.random(n) < 0.3] = 0
+    st = np.zeros(n, dtype=np.int64)
+    pos = 11
+    for i in range(n):
+        pos += int(gaps[i])
+        if i % 7 == 3:  # end this block on a row end
+            pos += (-(pos + int(lens[i]))) % 128
+        st[i] = pos
+        pos += int(lens[i])
+    data = stream_bytes(92, 0, pos + 64)
+    ext = np.stack([st, lens], 1).reshape(-1).astype(np.int64)
+    got = _u32(engine.crc32c_extents(_dev(torch, data), _dev(torch, ext)))
+    want = np.array([oracle.value(data[s:s + l].tobytes()) for s, l in zip(st, lens)], dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first blocks {bad[:8].tolist()}"
+
+
 def test_stream_verify_flags_flips(torch_cuda, oracle):
     from lsbm_amd import engine
     torch = torch_cuda

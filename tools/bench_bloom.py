@@ -286,7 +286,14 @@ def main():
                                     "+ 2 offset words + k byte + k_use probe bytes",
                       "members_found": found, "no_false_negatives": found == n})
     cpu = cpu_baseline(args.cpu_filters) if args.cpu_filters else None
+    # HBM bytes per launch from the PMC passes of tools/gpu_bloom_traffic.sh (same workload)
+    tp = os.path.join(REPO, "profiles", "bloom_traffic.json")
+    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
     for ln in lines:
+        t = traffic.get(ln["bench"], {}).get("traffic")
+        ln["roofline"]["traffic"] = int(t) if t else None
+        if t:
+            ln["roofline"]["traffic_over_algorithmic"] = round(t / ln["algorithmic_bytes"], 3)
         if cpu:
             ln["cpu_baseline"] = cpu
         print(json.dumps(ln), flush=True)
