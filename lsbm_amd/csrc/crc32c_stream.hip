@@ -71,7 +71,14 @@ __device__ unsigned long long g_stream_stats[16];
 
 constexpr uint32_t kSubBlocks = 63;   // blocks per sub-piece: one extent per lane; lane 63 always
                                       // holds the sentinel block that never starts or ends
-constexpr uint32_t kSlots = 1;        // block ends saved per group between flushes
+#ifndef LSBM_STREAM_PREISSUE  // (A/B builds override: 0 = load a sub-piece's first rows after the tail before)
+#define LSBM_STREAM_PREISSUE 1
+#endif
+#ifndef LSBM_STREAM_SLOTS  // (A/B builds override: 1 or 2)
+#define LSBM_STREAM_SLOTS 1
+#endif
+constexpr uint32_t kSlots = LSBM_STREAM_SLOTS;  // block ends saved per group between flushes
+static_assert(kSlots == 1 || kSlots == 2, "one or two slots");
 constexpr int kStreamAux = 2;         // buffer-load policy: non-temporal (read once)
 constexpr uint32_t kBank = 3;         // rows per load bank (two in flight); round-2 A/B on the
                                       // fixed kernel: 3-6 rows per bank alike
@@ -153,6 +160,67 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   // sub-piece starts without waiting for them.
   ExtRaw nx = {0, 0};
   uint64_t nx_b = ~0ull;  // nx holds the raw extents of blocks nx_b + lane
+  // The sub-piece of blocks b0 + lane (lane < navail) from their raw extents:
+  // this lane's extent, and (wave-uniform) the sub-piece's block count nb (0:
+  // the first block alone spans >= 2 GiB), row base pb, descriptor window
+  // [desc, desc + nrec) and rows NR.
+  struct Plan {
+    uint64_t sa, ea, bj;
+    bool fits;
+    uint64_t pb, desc;
+    uint32_t nb, nrec, NR;
+  };
+  auto plan = [&](uint64_t b0, uint32_t navail, const ExtRaw& rq) -> Plan {
+    Plan p;
+    const bool vq = lane < navail;
+    p.bj = vq ? b0 + lane : b0;
+    uint64_t at;
+    extent_from_raw(args, p.bj, rq, p.sa, p.ea, p.fits, at);
+    // a record that does not fit is empty and bad; a well-formed batch
+    // has such records only at its end, where the image ends
+    if (!p.fits) p.sa = p.ea = base + args.limit;
+    const uint64_t s_first = readlane64(p.sa, 0);
+    p.pb = s_first & ~127ull;  // the sub-piece's row base (absolute, 128-aligned)
+    // The sub-piece ends before the first block that is not in order (or
+    // overlaps the one before; offsets that go back make an empty block
+    // and then an earlier start) or that reaches 2 GiB past pb.
+    const uint64_t pe = shfl_up64(p.ea, 1);
+    bool cut = !vq || p.ea - p.pb >= (1ull << 31) - 4096u;  // (rows stay below the sentinel's)
+    if (lane > 0) cut = cut || p.sa < pe;
+    const uint64_t cm = __ballot(cut);
+    p.nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(cm ? (uint32_t)__builtin_ctzll(cm) : 64u));
+    const uint32_t last = p.nb ? p.nb - 1u : 0u;
+    const uint64_t e_last = readlane64(p.ea, last), s_last = readlane64(p.sa, last);
+    p.desc = p.pb + ((uint32_t)(s_first - p.pb) & ~15u);  // chunks in [desc, roundup16(e_last)) are read
+    p.nrec = (uint32_t)(((e_last + 15u) & ~15ull) - p.desc);
+    p.NR = end_row((uint32_t)(s_last - p.pb), (uint32_t)(e_last - p.pb)) + 1u;
+    // (wave-uniform: readfirstlane keeps the descriptor in SGPRs, with no
+    // waterfall loop around the loads)
+    p.desc = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p.desc) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p.desc >> 32)) << 32);
+    p.nrec = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.nrec);
+    p.pb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p.pb) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p.pb >> 32)) << 32);
+    p.NR = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.NR);
+    return p;
+  };
+  // Rows of a sub-piece: lane group g streams segment g of Q = ceil(NR / 8)
+  // rows, one 16-B chunk per lane, two banks of kBank rows in flight.  Rows
+  // past the segment are not read (the loop's last reloads, up to two banks
+  // per group, would otherwise fetch the next group's rows again -- ~7% more
+  // HBM reads on WAL records; an offset past the descriptor reads zeros
+  // without a memory access).
+  auto rows_of = [&](const Plan& p, uint32_t& Q, uint32_t& voff, __amdgpu_buffer_rsrc_t& rsrc) {
+    Q = (p.NR + 7u) >> 3;
+    voff = g * Q * (uint32_t)kRowBytes + 16u * li - (uint32_t)(p.desc - p.pb);  // (wraps: reads 0)
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(p.desc), (short)0, (int)p.nrec, 0x00020000);
+  };
+  auto ldr = [&](__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t Q, uint32_t r) -> u32x4 {
+    const uint32_t off = r < Q ? voff + r * (uint32_t)kRowBytes : 0x80000000u;
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, kStreamAux));
+  };
+  u32x4 ba[kBank], bb[kBank];
+  bool pre = false;  // the banks hold the next sub-piece's first rows already (issued before the tail)
   for (;;) {  // pieces (one, or this wave's range of every chunk)
     for (uint64_t b0 = b_lo; b0 < b_hi;) {
       // ---- the next sub-piece: up to 64 blocks in order (s_j >= e_{j-1}) ----
@@ -164,35 +232,19 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       uint32_t nrec, NR, nb;
       uint32_t aux = 0;  // this lane's block's expected / stored CRC or type byte (loaded now, used at the end)
       {
-        const bool vq = lane < navail;
-        const uint64_t bj = vq ? b0 + lane : b0;
         ExtRaw rq;
         if (nx_b == b0) {
           rq = nx;
         } else {
-          rq = load_ext_raw(args, bj);
+          rq = load_ext_raw(args, lane < navail ? b0 + lane : b0);
           if constexpr (kExt == kExtLogHeaders) log_length(args, rq);
         }
-        uint64_t sa, ea, at;
-        bool fits;
-        extent_from_raw(args, bj, rq, sa, ea, fits, at);
-        // a record that does not fit is empty and bad; a well-formed batch
-        // has such records only at its end, where the image ends
-        if (!fits) sa = ea = base + args.limit;
-        const uint64_t s_first = readlane64(sa, 0);
-        pb = s_first & ~127ull;  // the sub-piece's row base (absolute, 128-aligned)
-        // The sub-piece ends before the first block that is not in order (or
-        // overlaps the one before; offsets that go back make an empty block
-        // and then an earlier start) or that reaches 2 GiB past pb.
-        const uint64_t pe = shfl_up64(ea, 1);
-        bool cut = !vq || ea - pb >= (1ull << 31) - 4096u;  // (rows stay below the sentinel's)
-        if (lane > 0) cut = cut || sa < pe;
-        const uint64_t cm = __ballot(cut);
-        nb = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
-        nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)nb);
+        const Plan P = plan(b0, navail, rq);
+        nb = P.nb;
         if (nb == 0u) {  // the first block alone spans >= 2 GiB
           huge = true;
           b0 += 1;
+          pre = false;
           continue;
         }
         if (nb < kSubBlocks / 4u && nb < navail) {
@@ -202,12 +254,14 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           huge = true;
           break;
         }
-        const uint64_t e_last = readlane64(ea, nb - 1u), s_last = readlane64(sa, nb - 1u);
-        desc = pb + ((uint32_t)(s_first - pb) & ~15u);  // chunks in [desc, roundup16(e_last)) are read
-        nrec = (uint32_t)(((e_last + 15u) & ~15ull) - desc);
+        pb = P.pb;
+        desc = P.desc;
+        nrec = P.nrec;
+        NR = P.NR;
+        const uint64_t sa = P.sa, ea = P.ea, bj = P.bj;
+        const bool fits = P.fits;
         sr = lane < nb ? (uint32_t)(sa - pb) : 0x7fffff00u;
         er = lane < nb ? (uint32_t)(ea - pb) | (fits ? 0u : 0x80000000u) : 0x7fffff00u;
-        NR = end_row((uint32_t)(s_last - pb), (uint32_t)(e_last - pb)) + 1u;
         // the stored / written checksum: after the type byte, or in the log
         // header (6 bytes before the record's CRC bytes)
         const bool mine = lane < nb;
@@ -220,14 +274,6 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         if constexpr (kMode == kModeSstCrc) aux = *reinterpret_cast<gptr_u8>(q);
         if constexpr (kMode == kModeSstVerify || kMode == kModeLogVerify) aux = *reinterpret_cast<gptr_u32u>(q);
       }
-      // (wave-uniform: readfirstlane keeps the descriptor in SGPRs, with no
-      // waterfall loop around the loads)
-      desc = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)desc) |
-             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(desc >> 32)) << 32);
-      nrec = (uint32_t)__builtin_amdgcn_readfirstlane((int)nrec);
-      pb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pb) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pb >> 32)) << 32);
-      NR = (uint32_t)__builtin_amdgcn_readfirstlane((int)NR);
       nx_b = b0 + nb;
       if (nx_b < b_hi) {  // (clamped as above)
         const uint64_t na = b_hi - nx_b < kSubBlocks ? b_hi - nx_b : kSubBlocks;
@@ -235,10 +281,10 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       } else {
         nx_b = ~0ull;
       }
-      const __amdgpu_buffer_rsrc_t rsrc =
-          __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(desc), (short)0, (int)nrec, 0x00020000);
-      const uint32_t Q = (NR + 7u) >> 3;  // rows per segment
-      const uint32_t seg0 = g * Q;        // this group's first row (relative to pb)
+      uint32_t Q, voff;  // rows per segment; this lane's first chunk in the descriptor
+      __amdgpu_buffer_rsrc_t rsrc;
+      rows_of(Plan{0, 0, 0, true, pb, desc, nb, nrec, NR}, Q, voff, rsrc);
+      const uint32_t seg0 = g * Q;  // this group's first row (relative to pb)
       // the first block of this group's segment: the number of blocks that
       // end before it; and the group where this lane's block ends (its lane 0:
       // the block's raw CRC is delivered from there)
@@ -279,17 +325,20 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
       // saved block ends: braids and block (relative to b0)
       uint32_t cnt = 0;
-      uint32_t sx0[4] = {0, 0, 0, 0};
-      uint32_t sb0 = 0;
+      uint32_t sx0[4] = {0, 0, 0, 0}, sx1[4] = {0, 0, 0, 0};
+      uint32_t sb0 = 0, sb1 = 0;
 
       auto flush = [&]() {  // every lane active: merge and finish the saved blocks
         LSBM_TIC(2);
         LSBM_STAT(4, 1u);
-        if (__ballot(cnt != 0u) != 0ull) {
+#pragma unroll 1
+        for (uint32_t j = 0; j < kSlots; j++) {
+          if (__ballot(cnt > j) == 0ull) break;
           LSBM_STAT(5, 1u);
-          const uint32_t X = merge_braids(g_lds, sx0[0], sx0[1], sx0[2], sx0[3], lane_fin);
+          const uint32_t X = merge_braids(g_lds, j ? sx1[0] : sx0[0], j ? sx1[1] : sx0[1],
+                                          j ? sx1[2] : sx0[2], j ? sx1[3] : sx0[3], lane_fin);
           // lane l takes the CRC of block l from the group where it ends
-          const uint32_t bj = cnt != 0u ? sb0 : ~0u;
+          const uint32_t bj = cnt > j ? (j ? sb1 : sb0) : ~0u;
           const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
           const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
           if (bd == lane) px = xd;
@@ -297,16 +346,23 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         cnt = 0;
         LSBM_TOC(2);
       };
-      static_assert(kSlots == 1, "one slot");
       // Save braids x of block b, which ends in this row, into the group's
-      // slot (ends: group-uniform; the caller made room).
+      // next slot (ends: group-uniform; the caller made room).
       auto save = [&](bool ends, uint32_t b, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
-        sx0[0] = ends ? x0 : sx0[0];
-        sx0[1] = ends ? x1 : sx0[1];
-        sx0[2] = ends ? x2 : sx0[2];
-        sx0[3] = ends ? x3 : sx0[3];
-        sb0 = ends ? b : sb0;
-        cnt = ends ? 1u : cnt;
+        const bool s0 = ends && (kSlots == 1 || cnt == 0u), s1 = kSlots == 2 && ends && cnt == 1u;
+        sx0[0] = s0 ? x0 : sx0[0];
+        sx0[1] = s0 ? x1 : sx0[1];
+        sx0[2] = s0 ? x2 : sx0[2];
+        sx0[3] = s0 ? x3 : sx0[3];
+        sb0 = s0 ? b : sb0;
+        if constexpr (kSlots == 2) {
+          sx1[0] = s1 ? x0 : sx1[0];
+          sx1[1] = s1 ? x1 : sx1[1];
+          sx1[2] = s1 ? x2 : sx1[2];
+          sx1[3] = s1 ? x3 : sx1[3];
+          sb1 = s1 ? b : sb1;
+        }
+        cnt += ends ? 1u : 0u;
       };
       auto km = [&](uint32_t lo, uint32_t hi) -> u32x4 {  // bytes [lo, hi) of a chunk
         return *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + km_entry(lo, hi) * 16u);
@@ -325,22 +381,29 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // at its row start (A^-(S mod 128)(~0), util/crc32c.cc:289; lanes 1-7 of
       // a group read a zero word, the empty mask), En / Sn = the pointers'
       // next values.
-      uint32_t nev;
+      // erow: block ep's last row while it is open (~0 otherwise), srow: block
+      // sp's first row, nev: the nearer of the two
+      uint32_t nev, erow, srow;
       u32x4 mE, mS;
       uint32_t iv, En, Sn;
+      // (the init register's LDS address: lane 0 of a group reads R0[S mod 128],
+      // lanes 1-7 the zero word of the empty mask)
+      const uint32_t iv_base = li == 0u ? kStreamR0 : kStreamHM + km_entry(16u, 16u) * 16u;
+      const uint32_t iv_mask = li == 0u ? 127u : 0u;
       auto next_event = [&]() {
-        nev = min(sp != ep ? (E - 1u) >> 7 : ~0u, (S & ~kShort) >> 7);
+        erow = sp != ep ? (E - 1u) >> 7 : ~0u;
+        srow = (S & ~kShort) >> 7;
+        nev = min(erow, srow);
         const uint32_t rowa = nev * (uint32_t)kRowBytes + 16u * li;
         mE = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + clamp16(E, rowa) * 16u);
         mS = *reinterpret_cast<const u32x4*>(lds_c + kStreamHM + clamp16(S & ~kShort, rowa) * 16u);
-        iv = *reinterpret_cast<const uint32_t*>(
-            lds_c + (li == 0u ? kStreamR0 + (S & 127u) * 4u : kStreamHM + km_entry(16u, 16u) * 16u));
+        iv = *reinterpret_cast<const uint32_t*>(lds_c + iv_base + (S & iv_mask) * 4u);
         En = pick(ej, ep + 1u);
         Sn = pick(sxl, sp + 1u);
       };
       auto fix_lean = [&](u32x4 w, uint32_t rr) {  // after STEP_ROW: c = T(c) ^ w
-        const bool e_in = sp != ep && ((E - 1u) >> 7) == rr;
-        const bool s_in = ((S & ~kShort) >> 7) == rr;
+        const bool e_in = erow == rr;
+        const bool s_in = srow == rr;
         if (__ballot(e_in && cnt == kSlots) != 0ull) flush();
         LSBM_STAT(1, 1u);
         // block ep through E: T(c) ^ (w & bytes < E) = c ^ (w & mE)
@@ -402,16 +465,14 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       };
 
       // ---- the segment: half-steps of kBank rows, two banks in flight ----
-      const uint32_t voff = seg0 * (uint32_t)kRowBytes + 16u * li - (uint32_t)(desc - pb);  // (wraps: reads 0)
-      auto ld = [&](uint32_t r) -> u32x4 {
-        return __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + r * (uint32_t)kRowBytes, 0, kStreamAux));
-      };
-      u32x4 ba[kBank], bb[kBank];
+      auto ld = [&](uint32_t r) -> u32x4 { return ldr(rsrc, voff, Q, r); };
+      if (!pre) {
 #pragma unroll
-      for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
+        for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
 #pragma unroll
-      for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(kBank + k);
+        for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(kBank + k);
+      }
+      pre = false;
       next_event();
       // Rows are fixed up lean until one where some group's next block to
       // start is short; from there the rest of the bank goes through the
@@ -425,7 +486,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
             STEP_ROW(X[k]);
             LSBM_STAT(0, 1u);
             if (__ballot(nev == rr0 + k) != 0ull) {
-              const bool gen = ((S & ~kShort) >> 7) == rr0 + k && (S & kShort) != 0u;
+              const bool gen = srow == rr0 + k && (S & kShort) != 0u;
               if (__builtin_expect(__ballot(gen) != 0ull, 0)) k0 = k;
               else fix_lean(X[k], rr0 + k);
             }
@@ -458,6 +519,25 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       }
       LSBM_TOC(1);
       LSBM_TIC(5);
+      // ---- the next sub-piece's first rows, before this one's tail ----
+      // (its extents, and log record lengths, have arrived during the row
+      // loop; the tail's latency -- merges, a column load, the finishing chain
+      // -- then overlaps its first loads instead of leaving the wave with
+      // nothing in flight)
+      if (LSBM_STREAM_PREISSUE && nx_b != ~0ull) {
+        const uint32_t na = b_hi - nx_b < kSubBlocks ? (uint32_t)(b_hi - nx_b) : kSubBlocks;
+        const Plan P = plan(nx_b, na, nx);
+        if (P.nb != 0u && !(P.nb < kSubBlocks / 4u && P.nb < na)) {
+          uint32_t Q2, voff2;
+          __amdgpu_buffer_rsrc_t rsrc2;
+          rows_of(P, Q2, voff2, rsrc2);
+#pragma unroll
+          for (uint32_t k = 0; k < kBank; k++) ba[k] = ldr(rsrc2, voff2, Q2, k);
+#pragma unroll
+          for (uint32_t k = 0; k < kBank; k++) bb[k] = ldr(rsrc2, voff2, Q2, kBank + k);
+          pre = true;
+        }
+      }
       // ---- blocks that cross segments ----
       // T: the braids of the block still open at the segment end, shifted to
       // that block's last row; summed per block over consecutive groups, and

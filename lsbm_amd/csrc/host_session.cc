@@ -4,6 +4,8 @@
 #include <atomic>
 #include <chrono>
 
+#include <emmintrin.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -141,17 +143,58 @@ void parallel_for(size_t pieces, const std::function<void(size_t)>& fn) {
   if (pieces > 1) pool()->run(pieces, fn);
 }
 
-void parallel_copy(void* dst, const void* src, size_t n) {
-  constexpr size_t kPiece = 1u << 20;
-  if (n < (4u << 20)) {
-    memcpy(dst, src, n);
+// memcpy into a staging buffer with non-temporal stores: the pinned buffer is
+// only read again by the DMA engine, so its lines need not be read into the
+// cache first (a plain store to a line the cache does not hold reads it):
+// 2 host memory passes per byte instead of 3.  The pageable layers are bound
+// by this copy (profiles/r03/check1/host_timing.log: 38-43 GB/s with memcpy).
+// LSBM_HOST_COPY=plain keeps memcpy (A/B).
+namespace {
+bool plain_copy() {
+  static const bool plain = [] {
+    const char* v = getenv("LSBM_HOST_COPY");
+    return v && v[0] == 'p';
+  }();
+  return plain;
+}
+
+void stream_copy(char* d, const char* s, size_t n) {
+  if (n < 256 || plain_copy()) {
+    memcpy(d, s, n);
     return;
   }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+  memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
+  }
+  _mm_sfence();  // (the stores are visible before the DMA that follows is enqueued)
+  memcpy(d + i, s + i, n - i);
+}
+}  // namespace
+
+void parallel_copy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPiece = 1u << 20;
   char* d = static_cast<char*>(dst);
   const char* s = static_cast<const char*>(src);
+  if (n < (4u << 20)) {
+    stream_copy(d, s, n);
+    return;
+  }
   parallel_for((n + kPiece - 1) / kPiece, [&](size_t k) {
     const size_t off = k * kPiece;
-    memcpy(d + off, s + off, std::min(kPiece, n - off));
+    stream_copy(d + off, s + off, std::min(kPiece, n - off));
   });
 }
 
@@ -355,8 +398,10 @@ double HostTiming::now() {
 HostTiming::HostTiming(const char* w) : what(w), on(timing_on()), t0(on ? now() : 0.0) {}
 HostTiming::~HostTiming() {
   if (on)
-    fprintf(stderr, "{\"host_timing\": \"%s\", \"total_ms\": %.3f, \"copy_ms\": %.3f, \"wait_ms\": %.3f, \"post_ms\": %.3f}\n",
-            what, (now() - t0) * 1e3, t[kCopy] * 1e3, t[kWait] * 1e3, t[kPost] * 1e3);
+    fprintf(stderr, "{\"host_timing\": \"%s\", \"total_ms\": %.3f, \"copy_ms\": %.3f, \"wait_ms\": %.3f, \"post_ms\": %.3f, "
+            "\"prep_ms\": %.3f, \"enqueue_ms\": %.3f}\n",
+            what, (now() - t0) * 1e3, t[kCopy] * 1e3, t[kWait] * 1e3, t[kPost] * 1e3, t[kPrep] * 1e3,
+            t[kEnqueue] * 1e3);
 }
 
 bool host_fault_point(size_t enqueued) {

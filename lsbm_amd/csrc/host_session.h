@@ -161,16 +161,16 @@ void parallel_copy(void* dst, const void* src, size_t n);
 // Diagnostics (LSBM_HOST_TIMING=1 in the environment): a layer's pipeline
 // adds the wall time of its phases and prints one line to stderr per call:
 // the host copy into pinned staging, waits for a stage, the host-side result
-// handling, and the whole call.
+// handling, per-chunk metadata, the enqueue calls, and the whole call.
 struct HostTiming {
-  enum Phase { kCopy, kWait, kPost, kPhases };
+  enum Phase { kCopy, kWait, kPost, kPrep, kEnqueue, kPhases };
   explicit HostTiming(const char* what);
   ~HostTiming();
   void add(Phase p, double s) { t[p] += s; }
   static double now();
   const char* what;
   bool on;
-  double t0, t[kPhases] = {0, 0, 0};
+  double t0, t[kPhases] = {0, 0, 0, 0, 0};
 };
 
 // Fault injection for the error-path tests (lsbm_test_fail_host_pipeline):

@@ -42,18 +42,24 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
   };
   // windows of a multiple of kBlockSize, so that no record crosses one
   const uint64_t kLogChunk = HostSession::chunk_for(hi - lo) / kBlockSize * kBlockSize;
+  // (one search per window: a division per header cost ~10 ms per 1 GB log)
   std::vector<Chunk> chunks;
   for (size_t i = 0; i < n;) {
     const uint64_t w = heads[i] / kLogChunk;
-    Chunk c{std::max(lo, w * kLogChunk), std::min(hi, (w + 1) * kLogChunk), i, 0};
-    while (i < n && heads[i] / kLogChunk == w) i++, c.count++;
-    chunks.push_back(c);
+    const size_t j = (size_t)(std::lower_bound(heads + i, heads + n, (w + 1) * kLogChunk) - heads);
+    chunks.push_back(Chunk{std::max(lo, w * kLogChunk), std::min(hi, (w + 1) * kLogChunk), i, j - i});
+    i = j;
   }
   const bool pinned = host_pinned(img + lo, hi - lo);
   SessionLease s;
   Status st = s.Open(device);
   if (!st.ok()) return st;
   const size_t per = seal ? 4 : 1;
+  // the stages' buffers at their largest chunk's size, once: growing them
+  // chunk by chunk re-allocates page-locked memory mid-pipeline (a free that
+  // waits for the device; ~15 ms per 1 GB group commit)
+  size_t max_count = 0;
+  for (const Chunk& c : chunks) max_count = std::max(max_count, c.count);
   auto finish = [&](Stage& sg) -> Status {
     double t = tm.on ? HostTiming::now() : 0.0;
     const hipError_t e = s->wait(sg);
@@ -74,11 +80,13 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     const Chunk& c = chunks[k];
     const uint64_t bytes = c.hi - c.lo;
     hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
-    if (e == hipSuccess) e = sg.meta.reserve(c.count * sizeof(uint64_t));
-    if (e == hipSuccess) e = sg.res.reserve_mapped(c.count * per);  // (the kernel writes the host buffer)
+    if (e == hipSuccess) e = sg.meta.reserve(max_count * sizeof(uint64_t));
+    if (e == hipSuccess) e = sg.res.reserve_mapped(max_count * per);  // (the kernel writes the host buffer)
     if (e != hipSuccess) return hip_status(e, "staging buffers");
+    double tp = tm.on ? HostTiming::now() : 0.0;
     uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
     for (size_t i = 0; i < c.count; i++) hh[i] = heads[c.first + i] - c.lo;
+    if (tm.on) tm.add(HostTiming::kPrep, HostTiming::now() - tp);
     if (pinned) {
       e = hipMemcpyAsync(sg.bulk.d, img + c.lo, bytes, hipMemcpyHostToDevice, sg.stream);
     } else {
@@ -87,6 +95,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
       if (tm.on) tm.add(HostTiming::kCopy, HostTiming::now() - t);
       e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, bytes, hipMemcpyHostToDevice, sg.stream);
     }
+    tp = tm.on ? HostTiming::now() : 0.0;
     if (e == hipSuccess)
       e = hipMemcpyAsync(sg.meta.d, sg.meta.h, c.count * sizeof(uint64_t), hipMemcpyHostToDevice,
                          sg.stream);
@@ -98,6 +107,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
                                               sg.stream);
     if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
     e = hipEventRecord(sg.done, sg.stream);
+    if (tm.on) tm.add(HostTiming::kEnqueue, HostTiming::now() - tp);
     if (e != hipSuccess) return hip_status(e, "event");
     sg.busy = true;
     sg.tag = k;
@@ -341,6 +351,100 @@ void BatchWriter::AddRecord(const char* data, size_t n) {
   } while (n > 0);
 }
 
+// BatchReader::Verify's device pass, streamed: the image goes through the
+// stages in windows of whole 32 KiB log blocks, and each window's headers are
+// found by the same worker job that copies it into staging (2 MiB pieces: the
+// walk reads the caller's bytes the copy has just loaded, from cache), so the
+// header walk overlaps the previous windows' DMA and kernels instead of
+// preceding them all.  Appends every header from `first` on (ascending) to
+// *heads and its verdict to *ok.
+static Status verify_log_streamed(int device, const char* file, uint64_t size, uint64_t first,
+                           std::vector<uint64_t>* heads, std::vector<uint8_t>* ok) {
+  HostTiming tm("log_verify_streamed");
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(file);
+  const uint64_t kWin = HostSession::chunk_for(size - first) / kBlockSize * kBlockSize;
+  constexpr uint64_t kPiece = 64ull * kBlockSize;  // 2 MiB
+  const bool pinned = host_pinned(file + first, size - first);
+  SessionLease s;
+  Status st = s.Open(device);
+  if (!st.ok()) return st;
+  heads->reserve(heads->size() + (size - first) / 512);
+  struct Win {
+    uint64_t lo;
+    size_t first, count;
+  };
+  std::vector<Win> wins;
+  auto finish = [&](Stage& sg) -> Status {
+    double t = tm.on ? HostTiming::now() : 0.0;
+    const hipError_t e = s->wait(sg);
+    if (tm.on) tm.add(HostTiming::kWait, HostTiming::now() - t), t = HostTiming::now();
+    if (e != hipSuccess) return hip_status(e, "verify");
+    const Win& w = wins[sg.tag];
+    memcpy(ok->data() + w.first, sg.res.h, w.count);
+    if (tm.on) tm.add(HostTiming::kPost, HostTiming::now() - t);
+    return Status::OK();
+  };
+  std::vector<std::vector<uint64_t>> part((size_t)((kWin + kPiece - 1) / kPiece));
+  for (uint64_t lo = first, k = 0; lo < size; lo += kWin, k++) {
+    const uint64_t hi = std::min(size, lo + kWin);
+    Stage& sg = s->stage((int)(k % HostSession::kStages));
+    if (sg.busy) {
+      st = finish(sg);
+      if (!st.ok()) return st;
+    }
+    if (host_fault_point(k)) return Status::IOError("injected fault");  // (tests)
+    hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
+    if (e != hipSuccess) return hip_status(e, "staging buffers");
+    // copy (unless page-locked) and walk, piece by piece
+    const size_t np = (size_t)((hi - lo + kPiece - 1) / kPiece);
+    const double t0 = tm.on ? HostTiming::now() : 0.0;
+    parallel_for(np, [&](size_t q) {
+      const uint64_t p0 = lo + q * kPiece, p1 = std::min(hi, p0 + kPiece);
+      if (!pinned) parallel_copy(sg.bulk.h + (p0 - lo), file + p0, p1 - p0);  // (inline: nested)
+      part[q].clear();
+      for (uint64_t b = p0; b < p1; b += kBlockSize)
+        block_headers(img, b, std::min<uint64_t>(p1, b + kBlockSize), &part[q]);
+    });
+    if (tm.on) tm.add(HostTiming::kCopy, HostTiming::now() - t0);
+    const size_t first_h = heads->size();
+    for (size_t q = 0; q < np; q++) heads->insert(heads->end(), part[q].begin(), part[q].end());
+    const size_t count = heads->size() - first_h;
+    ok->resize(heads->size(), 0);
+    wins.push_back(Win{lo, first_h, count});
+    if (count == 0) continue;  // (nothing to check in this window: no stage work)
+    // (sized by the window's actual headers; the session keeps them, so they
+    // grow only while a call sees a denser window than any before)
+    e = sg.meta.reserve(count * sizeof(uint64_t));
+    if (e == hipSuccess) e = sg.res.reserve_mapped(count);
+    if (e != hipSuccess) return hip_status(e, "staging buffers");
+    uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
+    for (size_t i = 0; i < count; i++) hh[i] = (*heads)[first_h + i] - lo;
+    e = pinned ? hipMemcpyAsync(sg.bulk.d, file + lo, hi - lo, hipMemcpyHostToDevice, sg.stream)
+               : hipMemcpyAsync(sg.bulk.d, sg.bulk.h, hi - lo, hipMemcpyHostToDevice, sg.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(sg.meta.d, sg.meta.h, count * sizeof(uint64_t), hipMemcpyHostToDevice, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "H2D");
+    const int rc = lsbm_log_verify_dev(sg.bulk.d, hi - lo, reinterpret_cast<const uint64_t*>(sg.meta.d),
+                                       count, sg.res.d, nullptr, sg.stream);
+    if (rc != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
+    e = hipEventRecord(sg.done, sg.stream);
+    if (e != hipSuccess) return hip_status(e, "event");
+    sg.busy = true;
+    sg.tag = wins.size() - 1;
+  }
+  for (int i = 0; i < HostSession::kStages; i++) {  // (oldest first: tags ascend with the stage order)
+    Stage* oldest = nullptr;
+    for (int j = 0; j < HostSession::kStages; j++) {
+      Stage& sg = s->stage(j);
+      if (sg.busy && (!oldest || sg.tag < oldest->tag)) oldest = &sg;
+    }
+    if (!oldest) break;
+    st = finish(*oldest);
+    if (!st.ok()) return st;
+  }
+  return Status::OK();
+}
+
 Status BatchWriter::Seal(int device) {
   const size_t count = headers_.size() - sealed_;
   if (count == 0) return Status::OK();
@@ -378,36 +482,20 @@ Status BatchReader::Verify(int device) {
   delete walk_;
   walk_ = nullptr;
   headers_.clear();
-  {  // pass 1: every header the reader could check (all checksums assumed good).
-    // Records never cross a block (common/log_writer.cc:33-40) and the reader
-    // restarts at every block, so blocks are walked independently, in
-    // parallel: the reader's first block (log::Reader::SkipToInitialBlock,
-    // common/log_reader.cc:35-57) to the end of the file.
+  ok_.clear();
+  {  // pass 1: every header the reader could check (all checksums assumed good),
+    // and its verdict.  Records never cross a block (common/log_writer.cc:33-40)
+    // and the reader restarts at every block, so blocks are walked independently,
+    // window by window as the image streams to the device: the reader's first
+    // block (log::Reader::SkipToInitialBlock, common/log_reader.cc:35-57) to
+    // the end of the file.
     const uint64_t in_block = initial_offset_ % kBlockSize;
     uint64_t first = initial_offset_ - in_block;
     if (in_block > (uint64_t)kBlockSize - 6) first += kBlockSize;
     if (first < size_) {
-      constexpr uint64_t kPieceBlocks = 64;  // 2 MiB of log per piece
-      const uint64_t blocks = (size_ - first + kBlockSize - 1) / kBlockSize;
-      const size_t pieces = (size_t)((blocks + kPieceBlocks - 1) / kPieceBlocks);
-      std::vector<std::vector<uint64_t>> part(pieces);
-      parallel_for(pieces, [&](size_t k) {
-        const uint64_t b0 = first + k * kPieceBlocks * kBlockSize;
-        const uint64_t b1 = std::min<uint64_t>(size_, b0 + kPieceBlocks * kBlockSize);
-        part[k].reserve((b1 - b0) / 512);
-        for (uint64_t b = b0; b < b1; b += kBlockSize)
-          block_headers(img, b, std::min<uint64_t>(b1, b + kBlockSize), &part[k]);
-      });
-      size_t total = 0;
-      for (const auto& v : part) total += v.size();
-      headers_.reserve(total);
-      for (const auto& v : part) headers_.insert(headers_.end(), v.begin(), v.end());
+      Status s = verify_log_streamed(device, file_, size_, first, &headers_, &ok_);
+      if (!s.ok()) return s;
     }
-  }
-  ok_.assign(headers_.size(), 0);
-  if (!headers_.empty()) {  // one pipelined GPU pass over all of them
-    Status s = run_log(device, file_, 0, size_, headers_.data(), headers_.size(), false, ok_.data());
-    if (!s.ok()) return s;
   }
   // pass 2 (ReadRecord): the reader itself, with the GPU's verdicts
   walk_ = new Walk(img, size_, initial_offset_, reporter_, &headers_, &ok_);
