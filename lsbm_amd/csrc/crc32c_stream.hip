@@ -71,8 +71,8 @@ __device__ unsigned long long g_stream_stats[16];
 
 constexpr uint32_t kSubBlocks = 63;   // blocks per sub-piece: one extent per lane; lane 63 always
                                       // holds the sentinel block that never starts or ends
-#ifndef LSBM_STREAM_PREISSUE  // (A/B builds override: 0 = load a sub-piece's first rows after the tail before)
-#define LSBM_STREAM_PREISSUE 1
+#ifndef LSBM_STREAM_PREISSUE  // (A/B builds: 1 = issue the next sub-piece's first rows before the tail; measured -4.5 points on config 4, no gain on WAL: off)
+#define LSBM_STREAM_PREISSUE 0
 #endif
 #ifndef LSBM_STREAM_SLOTS  // (A/B builds override: 1 or 2)
 #define LSBM_STREAM_SLOTS 1
@@ -509,6 +509,9 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       // the first bank, and the loads queue behind the banks)
       if constexpr (kExt == kExtLogHeaders)
         if (nx_b != ~0ull) log_length(args, nx);
+      // (the reloads are not skipped past the segment: a branch around them
+      // makes the compiler's load counting merge pessimistically at the join,
+      // and WAL records lost 3-4 points; loads past the segment fetch nothing)
       for (uint32_t r = 0; r < Q; r += 2 * kBank) {
         half(ba, r);
 #pragma unroll
@@ -519,11 +522,21 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       }
       LSBM_TOC(1);
       LSBM_TIC(5);
+      // ---- blocks that cross segments ----
+      // T: the braids of the block still open at the segment end, shifted to
+      // that block's last row; summed per block over consecutive groups, and
+      // added to the block's CRC in the lane that finishes it.  (The column
+      // load first: the last flush hides its latency.)
+      const bool tvalid = sp != ep && ep < nb;
+      const uint32_t kt = tvalid ? ((E - 1u) >> 7) - (seg0 + Q - 1u) : 0u;  // rows to its last row
+      const u32x4 scols = *reinterpret_cast<gptr_u32x4>(
+          reinterpret_cast<uint64_t>(&dc->shift_cols[kt & (kShiftCols - 1u)][4 * li]));
       // ---- the next sub-piece's first rows, before this one's tail ----
       // (its extents, and log record lengths, have arrived during the row
-      // loop; the tail's latency -- merges, a column load, the finishing chain
-      // -- then overlaps its first loads instead of leaving the wave with
-      // nothing in flight)
+      // loop; the tail's latency -- merges, the finishing chain -- then
+      // overlaps its first loads instead of leaving the wave with nothing in
+      // flight.  Issued after the tail's column load, which the tail waits for:
+      // s_waitcnt counts vector loads in issue order)
       if (LSBM_STREAM_PREISSUE && nx_b != ~0ull) {
         const uint32_t na = b_hi - nx_b < kSubBlocks ? (uint32_t)(b_hi - nx_b) : kSubBlocks;
         const Plan P = plan(nx_b, na, nx);
@@ -538,15 +551,6 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           pre = true;
         }
       }
-      // ---- blocks that cross segments ----
-      // T: the braids of the block still open at the segment end, shifted to
-      // that block's last row; summed per block over consecutive groups, and
-      // added to the block's CRC in the lane that finishes it.  (The column
-      // load first: the last flush hides its latency.)
-      const bool tvalid = sp != ep && ep < nb;
-      const uint32_t kt = tvalid ? ((E - 1u) >> 7) - (seg0 + Q - 1u) : 0u;  // rows to its last row
-      const u32x4 scols = *reinterpret_cast<gptr_u32x4>(
-          reinterpret_cast<uint64_t>(&dc->shift_cols[kt & (kShiftCols - 1u)][4 * li]));
       flush();
       uint32_t xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
       xt = cols_apply(scols, xt, li);
