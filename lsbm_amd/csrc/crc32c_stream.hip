@@ -496,7 +496,11 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           LSBM_TIC(3);
 #pragma unroll 1
           for (uint32_t k = k0; k < kBank && r + k < Q; k++) {
-            const u32x4 w = k == 0 ? X[0] : (k == 1 || kBank == 2) ? X[1] : X[kBank - 1];
+            // (row k of the bank, k wave-uniform: a chain of selects, not an
+            // indexed private array, which would go to scratch)
+            const u32x4 w = k == 0 ? X[0] : k == 1 ? X[1 % kBank] : k == 2 ? X[2 % kBank]
+                          : k == 3 ? X[3 % kBank] : k == 4 ? X[4 % kBank] : X[5 % kBank];
+            static_assert(kBank <= 6, "rows of a bank: extend the select chain");
             if (k > k0) STEP_ROW(w);  // (row k0 has been stepped)
             fix_general(w, rr0 + k);
           }
