@@ -57,8 +57,8 @@ namespace lsbm {
 // diagnostic counters (tools/stream_stats.sh): wave-rows, slow wave-rows,
 // general half-steps, general iterations, flushes, slot merges, sub-pieces,
 // group events
-// and wave cycles in: sub-piece setup, row loop, flushes, general half-steps,
-// prepare, sub-piece tail
+// and wave cycles in: sub-piece setup, row loop, flushes, general rows, (4: unused),
+// sub-piece tail, the tail's per-lane finish (part of the tail)
 __device__ unsigned long long g_stream_stats[16];
 #define LSBM_STAT(i, v) (st[i] += (v))
 #define LSBM_TIC(i) const uint64_t tic_##i = __builtin_readcyclecounter()
@@ -572,6 +572,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fsrc - 32u), (int)key);
         if (fsrc != 0u && pk == lane) px ^= pv;
       }
+      LSBM_TIC(6);
       // ---- finish: lane l, block b0 + l ----
       {
         const bool mine = lane < nb;
@@ -615,6 +616,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           if (mine) args.ok[bi] = good ? 1u : 0u;
         }
       }
+      LSBM_TOC(6);
       LSBM_TOC(5);
       b0 += nb;
     }

@@ -108,7 +108,7 @@ def main():
         kib = d.numel() / 1024.0
         print(a.which, " ".join(f"{k}={v:.0f}" for k, v in st.items()))
         print(a.which, "per KiB:", " ".join(f"{k}={v / kib:.3f}" for k, v in st.items()))
-        tn = ["setup", "loop", "flush", "general", "prepare", "tail"]
+        tn = ["setup", "loop", "flush", "general", "unused", "tail", "finish(tail)"]
         tt = [buf[8 + i] / a.reps for i in range(len(tn))]
         tot = tt[0] + tt[1] + tt[5]
         print(a.which, "wave cycles %.3g:" % tot, " ".join(f"{k}={v / tot:.3f}" for k, v in zip(tn, tt)))
