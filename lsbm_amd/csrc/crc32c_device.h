@@ -156,4 +156,22 @@ __device__ __forceinline__ uint32_t merge_braids(const uint32_t* lds, uint32_t c
   return group_xor(u);
 }
 
+// Two independent merges at once (the stream kernel's tail: the last saved
+// block end and the segment's open block), their LDS lookups interleaved so
+// that one round trip's latency covers both chains.
+__device__ __forceinline__ void merge_braids2(const uint32_t* lds, uint32_t a0, uint32_t a1, uint32_t a2,
+                                              uint32_t a3, uint32_t b0, uint32_t b1, uint32_t b2,
+                                              uint32_t b3, uint32_t lane_fin, uint32_t& xa,
+                                              uint32_t& xb) {
+  uint32_t u = adv4_lds(lds, a0), v = adv4_lds(lds, b0);
+  u = adv4_lds(lds, u ^ a1);
+  v = adv4_lds(lds, v ^ b1);
+  u = adv4_lds(lds, u ^ a2);
+  v = adv4_lds(lds, v ^ b2);
+  u = fin_lds(lds, u ^ a3, lane_fin);
+  v = fin_lds(lds, v ^ b3, lane_fin);
+  xa = group_xor(u);
+  xb = group_xor(v);
+}
+
 }  // namespace lsbm

@@ -74,6 +74,12 @@ constexpr uint32_t kSubBlocks = 63;   // blocks per sub-piece: one extent per la
 #ifndef LSBM_STREAM_PREISSUE  // (A/B builds: 1 = issue the next sub-piece's first rows before the tail; measured -4.5 points on config 4, no gain on WAL: off)
 #define LSBM_STREAM_PREISSUE 0
 #endif
+#ifndef LSBM_STREAM_MERGE2  // (A/B builds: 0 = the tail flushes, then merges the open block)
+#define LSBM_STREAM_MERGE2 1
+#endif
+#ifndef LSBM_STREAM_EARLY_BANKS  // (A/B builds: 0 = a segment's first banks issued after the setup's picks)
+#define LSBM_STREAM_EARLY_BANKS 1
+#endif
 #ifndef LSBM_STREAM_SLOTS  // (A/B builds override: 1 or 2)
 #define LSBM_STREAM_SLOTS 1
 #endif
@@ -285,6 +291,16 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       __amdgpu_buffer_rsrc_t rsrc;
       rows_of(Plan{0, 0, 0, true, pb, desc, nb, nrec, NR}, Q, voff, rsrc);
       const uint32_t seg0 = g * Q;  // this group's first row (relative to pb)
+      // ---- the segment's first two banks: issued now, so that their memory
+      // latency runs under the rest of the setup (ballots, LDS picks) ----
+      auto ld = [&](uint32_t r) -> u32x4 { return ldr(rsrc, voff, Q, r); };
+      if (LSBM_STREAM_EARLY_BANKS && !pre) {
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
+#pragma unroll
+        for (uint32_t k = 0; k < kBank; k++) bb[k] = ld(kBank + k);
+        pre = true;
+      }
       // the first block of this group's segment: the number of blocks that
       // end before it; and the group where this lane's block ends (its lane 0:
       // the block's raw CRC is delivered from there)
@@ -465,7 +481,6 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       };
 
       // ---- the segment: half-steps of kBank rows, two banks in flight ----
-      auto ld = [&](uint32_t r) -> u32x4 { return ldr(rsrc, voff, Q, r); };
       if (!pre) {
 #pragma unroll
         for (uint32_t k = 0; k < kBank; k++) ba[k] = ld(k);
@@ -555,8 +570,21 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           pre = true;
         }
       }
-      flush();
-      uint32_t xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+      uint32_t xt;
+      static_assert(kSlots == 1 || !LSBM_STREAM_MERGE2, "the tail's paired merge takes one slot");
+      if constexpr (LSBM_STREAM_MERGE2) {
+        // the last saved ends and the open block's braids, merged together
+        uint32_t X;
+        merge_braids2(g_lds, sx0[0], sx0[1], sx0[2], sx0[3], c0, c1, c2, c3, lane_fin, X, xt);
+        const uint32_t bj = cnt != 0u ? sb0 : ~0u;
+        const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
+        const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
+        if (bd == lane) px = xd;
+        cnt = 0;
+      } else {
+        flush();
+        xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+      }
       xt = cols_apply(scols, xt, li);
       if (tvalid && kt >= kShiftCols) xt = shift_rows(g_lds, dc, xt, kt & ~(kShiftCols - 1u));
       uint32_t v = tvalid ? xt : 0u;
