@@ -344,22 +344,33 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       uint32_t sx0[4] = {0, 0, 0, 0}, sx1[4] = {0, 0, 0, 0};
       uint32_t sb0 = 0, sb1 = 0;
 
-      auto flush = [&]() {  // every lane active: merge and finish the saved blocks
+      // Merge every group's oldest saved end (one merge_braids for all 8
+      // groups) and hand each raw CRC to the lane of its block.  With two
+      // slots the slots are a FIFO: a group that must save a third end frees
+      // one slot in every group, so a merge takes the ends of most groups
+      // rather than only of those that happened to end a block lately.
+      auto merge_oldest = [&]() {  // every lane active
+        LSBM_STAT(5, 1u);
+        const uint32_t X = merge_braids(g_lds, sx0[0], sx0[1], sx0[2], sx0[3], lane_fin);
+        // lane l takes the CRC of block l from the group where it ends
+        const uint32_t bj = cnt != 0u ? sb0 : ~0u;
+        const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
+        const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
+        if (bd == lane) px = xd;
+        if constexpr (kSlots == 2) {
+          const bool two = cnt == 2u;
+          sx0[0] = two ? sx1[0] : sx0[0];
+          sx0[1] = two ? sx1[1] : sx0[1];
+          sx0[2] = two ? sx1[2] : sx0[2];
+          sx0[3] = two ? sx1[3] : sx0[3];
+          sb0 = two ? sb1 : sb0;
+        }
+        cnt = cnt != 0u ? cnt - 1u : 0u;
+      };
+      auto flush = [&]() {  // room for one more end in every group
         LSBM_TIC(2);
         LSBM_STAT(4, 1u);
-#pragma unroll 1
-        for (uint32_t j = 0; j < kSlots; j++) {
-          if (__ballot(cnt > j) == 0ull) break;
-          LSBM_STAT(5, 1u);
-          const uint32_t X = merge_braids(g_lds, j ? sx1[0] : sx0[0], j ? sx1[1] : sx0[1],
-                                          j ? sx1[2] : sx0[2], j ? sx1[3] : sx0[3], lane_fin);
-          // lane l takes the CRC of block l from the group where it ends
-          const uint32_t bj = cnt > j ? (j ? sb1 : sb0) : ~0u;
-          const uint32_t xd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)X);
-          const uint32_t bd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)fsrc, (int)bj);
-          if (bd == lane) px = xd;
-        }
-        cnt = 0;
+        if (__ballot(cnt != 0u) != 0ull) merge_oldest();
         LSBM_TOC(2);
       };
       // Save braids x of block b, which ends in this row, into the group's
@@ -571,7 +582,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         }
       }
       uint32_t xt;
-      static_assert(kSlots == 1 || !LSBM_STREAM_MERGE2, "the tail's paired merge takes one slot");
+      if constexpr (kSlots == 2 && LSBM_STREAM_MERGE2)  // (the paired merge takes the last one)
+        if (__ballot(cnt == 2u) != 0ull) merge_oldest();
       if constexpr (LSBM_STREAM_MERGE2) {
         // the last saved ends and the open block's braids, merged together
         uint32_t X;
@@ -582,7 +594,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         if (bd == lane) px = xd;
         cnt = 0;
       } else {
-        flush();
+        while (__ballot(cnt != 0u) != 0ull) merge_oldest();
         xt = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
       }
       xt = cols_apply(scols, xt, li);
