@@ -9,7 +9,7 @@
 // streamed regardless of block boundaries:
 //
 //   * a wave takes a piece of consecutive blocks (as the units kernel) and
-//     cuts it into sub-pieces of at most 64 blocks, whose extents it loads
+//     cuts it into sub-pieces of at most 63 blocks, whose extents it loads
 //     into registers (one per lane) and checks: ascending and non-overlapping
 //     (s_j >= e_{j-1}), within a 2 GiB window; a sub-piece ends before the
 //     first block that is not.  When that leaves fewer than 16 blocks (blocks
@@ -21,16 +21,21 @@
 //     load per lane per 128-B row through a buffer descriptor bounded to the
 //     sub-piece (chunks outside it read zeros), the braids c_m = A^128(c_m)
 //     ^ w_m (util/crc32c.cc:295-302 for a 128-B stride);
-//   * a row that holds a block boundary of its group takes the slow path:
-//     the bytes of the row that belong to the open block are kept (a 16-B
-//     mask from LDS), the block's braids are saved into a slot when it ends,
-//     the next block starts from zero braids with its init register ~0
-//     injected as A^-(s mod 128)(~0) at the row start (an LDS table), so that
-//     the register is exactly ~0 when its first byte is absorbed (:289);
-//   * when a group's two slots cannot take the block ends of the next rows,
-//     the slots are merged (merge_braids, lock-step over the groups) and each
-//     raw CRC goes to the lane of its block (block j of the sub-piece: lane j)
-//     by one ds_bpermute from the group where it ends;
+//   * every row is the plain row step; a row where some group starts or ends
+//     a block is then fixed up, as selects every group runs (a group-uniform
+//     branch here cost ~100 instructions and three dependent LDS round trips
+//     per such row, and on WAL records most rows are such rows): the ending
+//     block's braids through its end (a 16-B byte mask) are saved into the
+//     group's slot, the starting block's braids become its bytes of the row
+//     with its init register ~0 injected as A^-(s mod 128)(~0) (an LDS table),
+//     so that the register is exactly ~0 when its first byte is absorbed
+//     (:289).  The masks, the init word and the pointers' next values are read
+//     when the previous event was handled.  A row where a group starts and
+//     ends the same block goes through a general fix-up loop;
+//   * when a group must save an end while its slot is full, every group's
+//     oldest saved end is merged (merge_braids, one call for all 8 groups) and
+//     each raw CRC goes to the lane of its block (block j of the sub-piece:
+//     lane j) by one ds_bpermute from the group where it ends;
 //   * at the sub-piece end every lane finishes its own block: A^-z (z = the
 //     bytes after e in its last row) from the LDS power tables, the mode
 //     (CRC, masked CRC, verify, SSTable trailer CRC / check, log header seal /
