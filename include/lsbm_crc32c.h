@@ -116,10 +116,11 @@ int lsbm_crc32c_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64
  * file_bytes (include/lsbm/table_checksum.h does). */
 /* WriteRawBlock (table/table_builder.cc:237-255): write each trailer, with
  * type = d_types[i] (CompressionType, include/leveldb/options.h:24-29).
- * Two launches on the stream: the CRCs into 4 * n_blocks bytes of
+ * One launch on the stream: the CRCs into 4 * n_blocks bytes of
  * stream-ordered scratch (hipMallocAsync from the device's default pool,
- * which lsbm_crc32c_init() sets to keep freed memory), then the trailers
- * (in one pass if that scratch cannot be had). */
+ * which lsbm_crc32c_init() sets to keep freed memory), after which each wave
+ * merges its own blocks' trailers (written in place as they are computed if
+ * that scratch cannot be had, e.g. under graph capture). */
 int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
                       const uint8_t* d_types, uint64_t n_blocks, uint32_t* d_nbad, void* stream);
 /* The same trailers without touching the image: d_masked[i] =

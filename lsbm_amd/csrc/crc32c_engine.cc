@@ -529,14 +529,14 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   a.n = n_blocks;
   a.nbad = d_nbad;
   a.limit = file_bytes;
-  // Two passes: the CRCs densely into stream-ordered scratch (the read-
-  // streaming units kernel at full speed), then the trailers merged in by a
-  // compare-and-swap pass (trailer_scatter_kernel; DESIGN.md section 4:
-  // trailer writes interleaved with the reads cost 13 points).  Without
-  // scratch: in place, one pass.
-  // Small batches stay one pass: the second launch and the scratch cost a
-  // fixed ~10 us, the two passes save ~0.13 us per block (config 1's 45K
-  // blocks: 0.088 ms one pass, 0.099 ms two).
+  // The CRCs densely into stream-ordered scratch (the read-streaming units
+  // kernel at full speed), then the trailers merged in by compare-and-swap,
+  // per wave after its last row (trailer writes
+  // interleaved with the reads cost 13 points).  Without scratch: in place,
+  // one pass.
+  // Small batches stay one pass: the scratch (and, in round 2, the second
+  // launch) cost a fixed ~10 us, the deferred trailers save ~0.13 us per
+  // block (config 1's 45K blocks: 0.088 ms one pass, 0.099 ms two).
   // Under hipGraph capture: one pass as well (no stream-ordered allocation
   // inside a captured sequence; an unknown capture state counts as capturing).
   uint32_t* crcs = nullptr;
@@ -552,8 +552,13 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   }
   a.out = crcs;
   a.mode = kModeSstCrc;
+  // Each wave merges its own blocks' trailers after its last row (the units
+  // kernel's SstCrc epilogue, a.file set); LSBM_SEAL_SCATTER=1 keeps round 2's
+  // separate compare-and-swap pass (A/B).
+  static const bool scatter_pass = getenv("LSBM_SEAL_SCATTER") != nullptr;
+  if (!scatter_pass) a.file = d_file;
   rc = run_ragged(a, s);
-  if (rc == LSBM_OK) {
+  if (rc == LSBM_OK && scatter_pass) {
     const hipError_t e = launch_trailer_scatter(d_file, file_bytes, d_handles, d_types, crcs, n_blocks,
                                                 st->num_cus * 8, s);
     if (e != hipSuccess) rc = fail_hip(e, "trailer_scatter_kernel");

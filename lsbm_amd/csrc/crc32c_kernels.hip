@@ -173,17 +173,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 // Ragged path (crc32c_units.h): the units kernel walks each wave's range of
 // blocks in rounds of 8 units.
 // ---------------------------------------------------------------------------
-template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
-__global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
-  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
-                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
-  bool chunked;
-  uint32_t pi, p_end;
-  uint64_t b_lo, b_hi;
-  wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
-  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
-}
 
 // ---------------------------------------------------------------------------
 // Trailer scatter: the second pass of lsbm_sst_seal_dev.  The units kernel
@@ -232,6 +221,39 @@ __global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restric
     const uint64_t off = handles[2 * i], size = handles[2 * i + 1];
     if (!(off <= limit && limit - off >= kTrailer && limit - off - kTrailer >= size)) continue;
     merge_bytes(img, limit, img + off + size, 5, (uint64_t)types[i] | ((uint64_t)crcs[i] << 8));
+  }
+}
+
+// The units kernel; in SstCrc mode with args.file set (lsbm_sst_seal_dev) each
+// wave then merges the trailers of its own blocks into the image, from the
+// dense CRCs it has just written: the seal's trailer writes happen after the
+// wave's last row load (none of them queues in front of its reads) and
+// overlap the other waves' streaming, instead of a second pass over the
+// trailers after the kernel.
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWg;
+  bool chunked;
+  uint32_t pi, p_end;
+  uint64_t b_lo, b_hi;
+  wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
+  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
+  if constexpr (kMode == kModeSstCrc && kExt == kExtHandles) {
+    if (args.file != nullptr) {  // (SstCrc is never chunked: [b_lo, b_hi) is this wave's range)
+      // this wave's out[] stores complete (s_waitcnt vmcnt(0)) before it reads
+      // them back past L1 (an agent-scope fence would write back the whole L2)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      const uint64_t img = reinterpret_cast<uint64_t>(args.file), limit = args.limit;
+      const uint32_t lane = threadIdx.x & 63u;
+      for (uint64_t i = b_lo + lane; i < b_hi; i += 64) {
+        const uint64_t off = args.handles[2 * i], size = args.handles[2 * i + 1];
+        if (!(off <= limit && limit - off >= kTrailer && limit - off - kTrailer >= size)) continue;
+        const uint32_t crc = __hip_atomic_load(args.out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        merge_bytes(img, limit, img + off + size, 5, (uint64_t)args.types[i] | ((uint64_t)crc << 8));
+      }
+    }
   }
 }
 

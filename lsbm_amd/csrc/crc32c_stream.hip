@@ -695,7 +695,7 @@ bool stream_eligible(const RaggedArgs& a) {
   switch (a.mode) {
     case kModeOut: return a.extents == kExtOffsets || a.extents == kExtHandles;
     case kModeVerify: return a.extents == kExtOffsets;
-    case kModeSstCrc:
+    case kModeSstCrc: return a.extents == kExtHandles && !a.file;  // (the fused seal: units kernel)
     case kModeSstVerify: return a.extents == kExtHandles;
     case kModeLogSeal:
     case kModeLogVerify: return a.extents == kExtLogHeaders;

@@ -760,9 +760,11 @@ def test_sst_handles_past_the_image(torch_cuda, oracle):
 def test_sst_seal_every_trailer_with_tiny_blocks(torch_cuda, oracle, seed, smax, n):
     """Every trailer of a table whose blocks are 0..smax bytes: all trailers
     and every byte between and after them must come out exactly right.  From
-    131,072 blocks on the seal is two passes, the second merging trailers by
-    compare-and-swap on 8-byte words that several tiny blocks' trailers share
-    (crc32c_kernels.hip trailer_scatter_kernel); below, one pass."""
+    131,072 blocks on, the CRCs go densely into scratch and every wave then
+    merges its own blocks' trailers by compare-and-swap on 8-byte words that
+    several tiny blocks' trailers share -- words that can straddle two waves'
+    ranges (crc32c_kernels.hip crc32c_units_kernel's SstCrc epilogue); below,
+    one pass."""
     torch = torch_cuda
     from lsbm_amd import table
     rng = np.random.default_rng(seed)
