@@ -611,9 +611,9 @@ __attribute__((visibility("default"))) int lsbm_log_seal_dev(uint8_t* d_log, uin
                                                              void* stream) {
   if (n_records == 0) return LSBM_OK;
   if (!d_log || !d_headers) return fail(LSBM_ERR_INVALID, "null pointer");
-  // In place, one pass: WAL records are short (~1.2 KB), and a separate
-  // compare-and-swap header pass as lsbm_sst_seal_dev takes costs more than
-  // the in-kernel header writes do (A/B on 415K records: 0.167 vs 0.155 ms).
+  // One launch: WAL records are short (~1.2 KB), and a separate header pass
+  // costs more than the in-kernel header writes do (A/B on 415K records:
+  // 0.167 vs 0.155 ms, round 2).
   RaggedArgs a = {};
   a.base = d_log;
   a.file = d_log;
@@ -624,7 +624,33 @@ __attribute__((visibility("default"))) int lsbm_log_seal_dev(uint8_t* d_log, uin
   a.out = d_masked;
   a.nbad = d_nbad;
   a.mode = kModeLogSeal;
-  return run_ragged(a, static_cast<hipStream_t>(stream));
+  // Deferred headers (stream kernel): the masked CRCs densely into d_masked,
+  // the header stores after each wave's last row -- 48.7-48.9% -> 49.6-49.7%
+  // of HBM peak on 415K records (profiles/r03/logdefer/).  Without d_masked
+  // the stores stay in place: stream-ordered scratch for the CRCs costs what
+  // deferring saves (48.4-48.7% vs 48.6-48.8%).  LSBM_LOG_DEFER=0 / 1 turns
+  // deferring off / on with scratch (A/B measurements).
+  static const int defer_env = [] {
+    const char* e = getenv("LSBM_LOG_DEFER");
+    return e ? atoi(e) : -1;
+  }();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (defer_env == 0 || (defer_env < 0 && !d_masked)) return run_ragged(a, s);
+  a.flags |= kFlagDeferHeaders;
+  if (d_masked) return run_ragged(a, s);
+  uint32_t* crcs = nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+  if (capturing || n_records < (1u << 17) ||
+      hipMallocAsync(reinterpret_cast<void**>(&crcs), n_records * sizeof(uint32_t), s) != hipSuccess) {
+    (void)hipGetLastError();
+    a.flags &= ~kFlagDeferHeaders;
+    return run_ragged(a, s);
+  }
+  a.out = crcs;
+  const int rc = run_ragged(a, s);
+  (void)hipFreeAsync(crcs, s);
+  return rc;
 }
 
 __attribute__((visibility("default"))) int lsbm_log_crcs_dev(const uint8_t* d_log,

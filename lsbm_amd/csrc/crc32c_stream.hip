@@ -650,7 +650,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         } else if constexpr (kMode == kModeLogSeal) {  // common/log_writer.cc:85-88
           nbad += (uint32_t)__builtin_popcountll(__ballot(mine && bad));
           const uint32_t val = mask_crc(crc);
-          if (mine && !bad && args.file) {  // header[0..4): one unaligned dword store
+          if (mine && !bad && args.file && !(args.flags & kFlagDeferHeaders)) {  // header[0..4): one unaligned dword store
             typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
             *reinterpret_cast<gu32u>(pb + sr - 6u) = val;
           }
@@ -684,6 +684,28 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     units_fallback<kFallbackRows, kMode, kExt>(
         (const RaggedArgs*)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
     return;
+  }
+  if constexpr (kMode == kModeLogSeal) {
+    // Deferred headers: this wave's masked CRCs went densely to out[] with
+    // its reads; the scattered header stores follow its last row, so they do
+    // not sit in the in-order load counter between the streamed rows (the
+    // SSTable seal's trailer epilogue, crc32c_kernels.hip).  (Not chunked:
+    // [b_lo, b_hi) is the wave's whole range.)
+    if ((args.flags & kFlagDeferHeaders) && args.file) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's out[] stores performed
+      typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
+      for (uint64_t i = b_lo + lane; i < b_hi; i += 64u) {
+        ExtRaw r = load_ext_raw(args, i);
+        log_length(args, r);
+        uint64_t s, e, at;
+        bool fits;
+        extent_from_raw(args, i, r, s, e, fits, at);
+        if (fits) {
+          const uint32_t v = __hip_atomic_load(args.out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *reinterpret_cast<gu32u>(reinterpret_cast<uint64_t>(args.file) + (at - base)) = v;  // header[0..4)
+        }
+      }
+    }
   }
   if (lane == 0u && nbad && args.nbad) atomicAdd(args.nbad, nbad);
 }

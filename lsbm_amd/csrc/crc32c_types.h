@@ -78,6 +78,10 @@ enum ExtentKind : uint32_t {
                        // length = LE16 at h + 4 (common/log_format.h, 7-byte header)
 };
 
+// RaggedArgs::flags bits besides the mask bit (1)
+constexpr uint32_t kFlagDeferHeaders = 2u;  // kModeLogSeal, stream kernel: out[] first, the headers
+                                            // after each wave's last row (out must be set)
+
 enum RaggedMode : uint32_t {
   kModeOut = 0,        // out[i] = crc (masked if flags & 1)
   kModeVerify = 1,     // ok[i] = (crc == expect[i]); mismatches added to *nbad

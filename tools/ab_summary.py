@@ -10,7 +10,7 @@ for f in sys.argv[1:]:
         d = json.loads(line)
         c = d["config"]
         if c == "wal":
-            r = {k: d[k]["pct_hbm_peak"] for k in ("log_seal", "log_crcs", "log_verify")}
+            r = {k: d[k]["pct_hbm_peak"] for k in ("log_seal", "log_seal_no_out", "log_crcs", "log_verify") if k in d}
         elif c == "sst4118":
             r = {"ext": d["pct_hbm_peak"], "seal": d["sst_seal"]["pct_hbm_peak"],
                  "tcrc": d["sst_trailer_crcs"]["pct_hbm_peak"], "verify": d["sst_verify"]["pct_hbm_peak"]}
