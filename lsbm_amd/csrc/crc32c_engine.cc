@@ -536,14 +536,19 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   // one pass.
   // Small batches stay one pass: the scratch (and, in round 2, the second
   // launch) cost a fixed ~10 us, the deferred trailers save ~0.13 us per
-  // block (config 1's 45K blocks: 0.088 ms one pass, 0.099 ms two).
+  // block (config 1's 45K blocks: 0.088 ms one pass, 0.099 ms two; round 3's
+  // per-wave merges: 0.092 one pass, 0.096 merged, profiles/r03/sealmin/).
   // Under hipGraph capture: one pass as well (no stream-ordered allocation
   // inside a captured sequence; an unknown capture state counts as capturing).
   uint32_t* crcs = nullptr;
   static const bool one_pass = getenv("LSBM_SEAL_ONE_PASS") != nullptr;  // (A/B measurements)
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
-  if (one_pass || capturing || n_blocks < (1u << 17) ||
+  static const uint64_t min_blocks = [] {  // (A/B measurements)
+    const char* e = getenv("LSBM_SEAL_MIN_BLOCKS");
+    return e ? strtoull(e, nullptr, 10) : (1ull << 17);
+  }();
+  if (one_pass || capturing || n_blocks < min_blocks ||
       hipMallocAsync(reinterpret_cast<void**>(&crcs), n_blocks * sizeof(uint32_t), s) != hipSuccess) {
     (void)hipGetLastError();
     a.file = d_file;
