@@ -435,6 +435,9 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 // leaves LDS once.  The round's key words are staged in the region's free
 // tail (wave_hash).  Otherwise the group's filters go one by one through
 // build_one.
+#ifndef LSBM_BUILD_DEPTH  // (A/B builds override)
+#define LSBM_BUILD_DEPTH 1
+#endif
 #ifndef LSBM_BUILD_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_BUILD_WAVES_PER_EU 7
 #endif
@@ -557,6 +560,19 @@ void bloom_build_kernel(BloomBuildArgs a) {
       plan = plan_span(kbase + oa0, n, avail, safe);
       fetch_span(plan, ch0, ch1);
     }
+#if LSBM_BUILD_DEPTH == 2
+    // (A/B: key words two rounds ahead, offsets three)
+    uint64_t oc0 = 0, oc1 = 0;
+    if (lane + 128u < nkeys) load_off2(ko, lane + 128, oc0, oc1);
+    SpanPlan plan2;
+    u32x4 ch2, ch3;
+    {
+      const bool act1 = lane + 64u < nkeys;
+      const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
+      plan2 = plan_span(kbase + ob0, n1, avail, safe);
+      fetch_span(plan2, ch2, ch3);
+    }
+#endif
     for (uint32_t r0 = 0; r0 < nkeys; r0 += 64) {  // wave-uniform rounds
       const uint32_t r = r0 + lane;
       const bool act = r < nkeys;
@@ -578,6 +594,22 @@ void bloom_build_kernel(BloomBuildArgs a) {
       // this round's chunks into LDS, then the next round's plan and loads
       const SpanPlan cur = plan;
       const u32x4 cc0 = ch0, cc1 = ch1;
+#if LSBM_BUILD_DEPTH == 2
+      plan = plan2;
+      ch0 = ch2;
+      ch1 = ch3;
+      {
+        const bool act2 = r + 128u < nkeys;
+        const uint64_t n2 = act2 && oc1 >= oc0 + a.strip ? oc1 - oc0 - a.strip : 0;
+        plan2 = plan_span(kbase + oc0, n2, avail, safe);
+        fetch_span(plan2, ch2, ch3);
+        oa0 = ob0;
+        oa1 = ob1;
+        ob0 = oc0;
+        ob1 = oc1;
+        if (r + 192u < nkeys) load_off2(ko, r + 192, oc0, oc1);
+      }
+#else
       {
         const bool act1 = r + 64u < nkeys;
         const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
@@ -587,6 +619,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
         oa1 = ob1;
         if (r + 128u < nkeys) load_off2(ko, r + 128, ob0, ob1);
       }
+#endif
       const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
       if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
