@@ -68,7 +68,7 @@ def main():
         offs = torch.arange(0, (n + 1) * ln, ln, dtype=torch.int64, device="cuda")
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         fn = lambda: engine.crc32c_batch(d, offs, out=out, stream=s)
-    elif a.which == "sst":
+    elif a.which in ("sst", "sstseal"):
         n, ln = 1 << 20, 4118
         offs = np.arange(n + 1, dtype=np.int64) * (ln + 5)
         d = torch.empty(int(offs[-1]) + 16, dtype=torch.uint8, device="cuda")
@@ -77,7 +77,10 @@ def main():
                                    .reshape(-1).copy()).to("cuda")
         types = torch.zeros(n, dtype=torch.uint8, device="cuda")
         table.seal_blocks(d, handles, types, stream=s)
-        fn = lambda: table.verify_blocks(d, handles, stream=s)
+        if a.which == "sst":
+            fn = lambda: table.verify_blocks(d, handles, stream=s)
+        else:  # lsbm_sst_seal_dev: dense CRCs + per-wave trailer merges
+            fn = lambda: table.seal_blocks(d, handles, types, stream=s)
     elif a.which == "c4":
         from bench_configs import zipf_lengths
         n = 2_000_000
