@@ -627,11 +627,20 @@ void bloom_build_kernel(BloomBuildArgs a) {
 #ifdef LSBM_PROBE_UNROLL  // A/B builds only
 #pragma unroll LSBM_PROBE_UNROLL
 #endif
+#ifdef LSBM_DIAG_NO_PROBE_WRITES  // (diagnostic A/B builds only: wrong filters)
+      uint32_t acc = 0;
+      for (uint32_t q = 0; q < a.k; q++) {
+        acc ^= bbase + ps.pos;
+        ps.next();
+      }
+      if (acc == 0xffffffffu) bm[0] = acc;
+#else
       for (uint32_t q = 0; q < a.k; q++) {
         const uint32_t b = bbase + ps.pos;
         atomicOr(&bm[b >> 5], 1u << (b & 31u));
         ps.next();
       }
+#endif
     }
     load_meta(grp + nwaves);
     wave_phase();

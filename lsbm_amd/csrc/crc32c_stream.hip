@@ -696,10 +696,13 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
       for (uint64_t i = b_lo + lane; i < b_hi; i += 64u) {
         ExtRaw r = load_ext_raw(args, i);
-        log_length(args, r);
-        uint64_t s, e, at;
-        bool fits;
-        extent_from_raw(args, i, r, s, e, fits, at);
+        uint64_t at = base + r.x;
+        bool fits = true;
+        if (nbad != 0u) {  // (only a wave with a record that does not fit reads the lengths again)
+          log_length(args, r);
+          uint64_t s, e;
+          extent_from_raw(args, i, r, s, e, fits, at);
+        }
         if (fits) {
           const uint32_t v = __hip_atomic_load(args.out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           *reinterpret_cast<gu32u>(reinterpret_cast<uint64_t>(args.file) + (at - base)) = v;  // header[0..4)
