@@ -201,10 +201,30 @@ int lsbm_stream_read_dev(const void* d_buf, uint64_t nbytes, uint32_t* d_sink, v
  * disarm).  Not for production use. */
 int lsbm_test_fail_host_pipeline(int chunks);
 /* Ragged-batch kernel policy (what LSBM_RAGGED_KERNEL sets at start-up): 0 the
- * default (the stream kernel for offsets[] batches, the units kernel for the
- * rest), 1 the units kernel for every batch, 2 the stream kernel for every
+ * default (the stream kernel for offsets[] batches and for log record headers,
+ * the units kernel for fixed-stride, {offset, length} extents and SSTable
+ * handles), 1 the units kernel for every batch, 2 the stream kernel for every
  * batch it takes.  Results are identical; for tests and A/B runs. */
 int lsbm_test_ragged_kernel(int which);
+
+/* ---- host runtime (the C++ layers' sessions and worker pool) ---- */
+/* Worker threads of the host pool: usable cores - 1, where usable cores = the
+ * affinity mask capped by the cgroup CPU quota (LSBM_HOST_THREADS overrides);
+ * starts the pool. */
+int lsbm_host_threads(void);
+/* NUMA node of HIP device `device` (from its PCI bus id and
+ * /sys/bus/pci/devices/<id>/numa_node), -1 if unknown. */
+int lsbm_device_numa_node(int device);
+/* Testing: the same lookup under another sysfs root; cpulist parsing ("0-3,8"
+ * -> up to cap CPUs, returns the count or -1 if malformed); the cgroup quota
+ * under another cgroup root (whole CPUs, 0 if none); and the pool under load:
+ * `callers` threads each run `jobs` parallel jobs of `pieces` pieces that each
+ * sleep `piece_us`; returns the most jobs that had pieces running at once and
+ * stores the wall seconds in *seconds. */
+int lsbm_test_pci_numa_node(const char* sysfs_root, const char* bus_id);
+int lsbm_test_parse_cpulist(const char* list, int* cpus, int cap);
+int lsbm_test_cgroup_quota(const char* cgroup_root);
+int lsbm_test_pool_overlap(int callers, int jobs, int pieces, int piece_us, double* seconds);
 
 #ifdef __cplusplus
 }  /* extern "C" */

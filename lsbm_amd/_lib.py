@@ -53,6 +53,12 @@ SIGNATURES = {
     "lsbm_stream_read_dev": (_int, [_vp, _u64, _vp, _vp]),
     "lsbm_test_fail_host_pipeline": (_int, [_int]),
     "lsbm_test_ragged_kernel": (_int, [_int]),
+    "lsbm_host_threads": (_int, []),
+    "lsbm_device_numa_node": (_int, [_int]),
+    "lsbm_test_pci_numa_node": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "lsbm_test_parse_cpulist": (_int, [ctypes.c_char_p, _vp, _int]),
+    "lsbm_test_cgroup_quota": (_int, [ctypes.c_char_p]),
+    "lsbm_test_pool_overlap": (_int, [_int, _int, _int, _int, _vp]),
     # include/lsbm_bloom.h
     "lsbm_bloom_hash": (_u32, [_vp, _sz, _u32]),
     "lsbm_bloom_filter_bytes": (_u64, [_u64, _int]),

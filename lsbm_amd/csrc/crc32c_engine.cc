@@ -22,6 +22,7 @@
 #include "crc32c_types.h"
 #include "engine_internal.h"
 #include "gf2.h"
+#include "host_numa.h"
 #include "host_session.h"
 
 namespace lsbm {
@@ -261,99 +262,6 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_units_kernel");
 }
 
-// ---- host-staged pipeline ----
-struct Slot {
-  uint8_t* h_data = nullptr;  // pinned
-  uint64_t* h_off = nullptr;  // pinned
-  uint32_t* h_init = nullptr;
-  uint32_t* h_out = nullptr;
-  uint8_t* d_data = nullptr;
-  uint64_t* d_off = nullptr;
-  uint32_t* d_init = nullptr;
-  uint32_t* d_out = nullptr;
-  uint64_t cap_bytes = 0, cap_blocks = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
-  // pending chunk
-  bool busy = false;
-  uint64_t first = 0, count = 0;
-};
-
-struct Staging {
-  std::mutex mu;
-  bool ready = false;
-  Slot slot[3];
-};
-Staging g_staging[kMaxDevices];
-
-void free_slot_buffers(Slot& s) {
-  if (s.h_data) hipHostFree(s.h_data);
-  if (s.h_off) hipHostFree(s.h_off);
-  if (s.h_init) hipHostFree(s.h_init);
-  if (s.h_out) hipHostFree(s.h_out);
-  if (s.d_data) hipFree(s.d_data);
-  if (s.d_off) hipFree(s.d_off);
-  if (s.d_init) hipFree(s.d_init);
-  if (s.d_out) hipFree(s.d_out);
-  s.h_data = nullptr; s.h_off = nullptr; s.h_init = nullptr; s.h_out = nullptr;
-  s.d_data = nullptr; s.d_off = nullptr; s.d_init = nullptr; s.d_out = nullptr;
-  s.cap_bytes = s.cap_blocks = 0;
-}
-
-hipError_t reserve_slot(Slot& s, uint64_t bytes, uint64_t blocks) {
-  if (!s.stream) {
-    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-    if (e != hipSuccess) return e;
-    e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-  }
-  if (bytes <= s.cap_bytes && blocks <= s.cap_blocks) return hipSuccess;
-  free_slot_buffers(s);
-  bytes = std::max<uint64_t>(bytes, 64ull << 20);
-  blocks = std::max<uint64_t>(blocks, 1ull << 16);
-  hipError_t e;
-  if ((e = hipHostMalloc((void**)&s.h_data, bytes, hipHostMallocDefault)) != hipSuccess) return e;
-  if ((e = hipHostMalloc((void**)&s.h_off, (blocks + 1) * 8, hipHostMallocDefault)) != hipSuccess)
-    return e;
-  if ((e = hipHostMalloc((void**)&s.h_init, blocks * 4, hipHostMallocDefault)) != hipSuccess)
-    return e;
-  if ((e = hipHostMalloc((void**)&s.h_out, blocks * 4, hipHostMallocDefault)) != hipSuccess)
-    return e;
-  if ((e = hipMalloc(&s.d_data, bytes)) != hipSuccess) return e;
-  if ((e = hipMalloc(&s.d_off, (blocks + 1) * 8)) != hipSuccess) return e;
-  if ((e = hipMalloc(&s.d_init, blocks * 4)) != hipSuccess) return e;
-  if ((e = hipMalloc(&s.d_out, blocks * 4)) != hipSuccess) return e;
-  s.cap_bytes = bytes;
-  s.cap_blocks = blocks;
-  return hipSuccess;
-}
-
-// Copy blocks [first, last) of a pageable source into the pinned staging
-// buffer at their rebased offsets, on up to 8 threads for large chunks.
-void gather_blocks(uint8_t* dst, const uint64_t* rebased, const uint8_t* src,
-                   const uint64_t* offsets, uint64_t first, uint64_t last) {
-  auto copy_range = [&](uint64_t lo, uint64_t hi) {
-    for (uint64_t i = lo; i < hi; i++) {
-      const uint64_t s0 = offsets[i], s1 = offsets[i + 1];
-      if (s1 > s0) memcpy(dst + rebased[i - first], src + s0, s1 - s0);
-    }
-  };
-  const uint64_t bytes = rebased[last - first];
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nt = bytes < (8u << 20) ? 1u : std::min(8u, hw);
-  if (nt == 1) {
-    copy_range(first, last);
-    return;
-  }
-  std::vector<std::thread> th;
-  const uint64_t per = (last - first + nt - 1) / nt;
-  for (unsigned t = 0; t < nt; t++) {
-    const uint64_t lo = std::min(last, first + t * per), hi = std::min(last, lo + per);
-    if (lo < hi) th.emplace_back(copy_range, lo, hi);
-  }
-  for (auto& t : th) t.join();
-}
-
 }  // namespace
 
 // engine_internal.h: shared with the bloom entry points (bloom_engine.cc)
@@ -386,8 +294,8 @@ __attribute__((visibility("default"))) int lsbm_crc32c_init(int device) {
 }
 
 __attribute__((visibility("default"))) int lsbm_crc32c_shutdown(void) {
-  // the C++ layers' staging first (it synchronises its streams), then the
-  // host-staged batch slots and the per-device tables
+  // the sessions' staging first (it synchronises their streams), then the
+  // per-device tables
   HostSession::ShutdownAll();
   int prev = 0;
   const bool have_prev = hipGetDevice(&prev) == hipSuccess;
@@ -395,19 +303,10 @@ __attribute__((visibility("default"))) int lsbm_crc32c_shutdown(void) {
   for (int dev = 0; dev < kMaxDevices; dev++) {
     DeviceState* st = &g_dev[dev];
     std::lock_guard<std::mutex> l(st->mu);
-    Staging& stg = g_staging[dev];
-    std::lock_guard<std::mutex> ls(stg.mu);
     if (!st->ready.load()) continue;
     if (hipSetDevice(dev) != hipSuccess) {
       rc = fail(LSBM_ERR_HIP, "hipSetDevice");
       continue;
-    }
-    for (Slot& sl : stg.slot) {
-      if (sl.stream) (void)hipStreamSynchronize(sl.stream);
-      free_slot_buffers(sl);
-      if (sl.done) (void)hipEventDestroy(sl.done);
-      if (sl.stream) (void)hipStreamDestroy(sl.stream);
-      sl = Slot();
     }
     (void)hipDeviceSynchronize();  // no kernel may still read the tables
     if (st->d_consts) (void)hipFree(st->d_consts);
@@ -739,6 +638,13 @@ __attribute__((visibility("default"))) int lsbm_stream_read_dev(const void* d_bu
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "stream_read_kernel");
 }
 
+// The host-staged batch: chunks of whole blocks (<= 64 MiB, <= 64K blocks)
+// through a leased HostSession's stages (host_session.h: per-device sessions,
+// pinned staging on the device's NUMA node).  A chunk whose extents are in
+// order and tight in page-locked memory is DMA-ed in place; any other chunk
+// is gathered into the stage's pinned buffer by the worker pool, with its
+// rebased offsets and init values behind the bytes (one DMA).  The kernel
+// writes the CRCs straight into the stage's mapped host buffer.
 __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, const void* h_base,
                                                                   const uint64_t* h_offsets,
                                                                   uint64_t n_blocks,
@@ -751,12 +657,12 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
   DeviceState* st = nullptr;
   int rc = ensure_device(device, &st);
   if (rc != LSBM_OK) return rc;
-  int prev = 0;
-  hipGetDevice(&prev);
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
-  Staging& stg = g_staging[device];
-  std::lock_guard<std::mutex> lock(stg.mu);
+  SessionLease lease;
+  {
+    const Status os = lease.Open(device);
+    if (!os.ok()) return fail(LSBM_ERR_HIP, os.ToString().c_str());
+  }
+  HostSession& hs = *lease;
   const uint8_t* src = static_cast<const uint8_t*>(h_base);
   const bool src_pinned = host_pinned(h_base, 1);  // (each chunk's range is checked before its DMA)
   // chunk size: LSBM_STAGE_CHUNK_MB overrides (tuning only; tools/host_sweep.py)
@@ -766,22 +672,23 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
     return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 64) << 20;
   }();
   const uint64_t kChunkBlocks = kChunkBytes >> 10;
-  const int nslots = 3;
-  int si = 0;
-  uint64_t next = 0;
-  rc = LSBM_OK;
-
-  auto drain = [&](Slot& s) -> int {
+  const uint64_t meta_cap = (kChunkBlocks + 1) * 8 + kChunkBlocks * 4 + 512;
+  struct Pending {
+    uint64_t first = 0, count = 0;
+  };
+  Pending pend[HostSession::kStages];
+  auto drain = [&](int i) -> int {
+    Stage& s = hs.stage(i);
     if (!s.busy) return LSBM_OK;
-    hipError_t ee = hipEventSynchronize(s.done);
-    s.busy = false;
+    const hipError_t ee = hs.wait(s);
     if (ee != hipSuccess) return fail_hip(ee, "staged chunk");
-    memcpy(h_out + s.first, s.h_out, s.count * 4);
+    memcpy(h_out + pend[i].first, s.res.h, pend[i].count * 4);
     return LSBM_OK;
   };
-
+  uint64_t next = 0;
+  int si = 0;
   while (next < n_blocks && rc == LSBM_OK) {
-    // choose the chunk [next, last)
+    // the chunk [next, last)
     uint64_t bytes = 0, last = next;
     while (last < n_blocks && last - next < kChunkBlocks) {
       const uint64_t s0 = h_offsets[last], s1 = h_offsets[last + 1];
@@ -790,79 +697,97 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
       bytes += len;
       last++;
     }
-    Slot& s = stg.slot[si];
-    si = (si + 1) % nslots;
-    rc = drain(s);
-    if (rc != LSBM_OK) break;
-    e = reserve_slot(s, bytes + 16, last - next);
+    const int i = si;
+    si = (si + 1) % HostSession::kStages;
+    Stage& s = hs.stage(i);
+    if ((rc = drain(i)) != LSBM_OK) break;
+    const uint64_t cnt = last - next;
+    hipError_t e = s.bulk.reserve(std::max<uint64_t>(kChunkBytes, bytes) + meta_cap);
+    if (e == hipSuccess) e = s.res.reserve_mapped(std::max<uint64_t>(kChunkBlocks, cnt) * 4);
     if (e != hipSuccess) {
       rc = fail_hip(e, "staging buffers");
       break;
     }
     // rebased offsets; a chunk whose extents are in order and tight can be
-    // DMA-ed straight from a pinned source, otherwise it is gathered
-    const uint64_t cnt = last - next;
-    uint64_t pos = 0;
+    // DMA-ed straight from a page-locked source, otherwise it is gathered
     bool tight = src_pinned;
-    for (uint64_t i = next; i < last; i++) {
-      const uint64_t s0 = h_offsets[i], s1 = h_offsets[i + 1];
-      const uint64_t len = s1 > s0 ? s1 - s0 : 0;
+    uint64_t pos = 0;
+    for (uint64_t k = next; k < last && tight; k++) {
+      const uint64_t s0 = h_offsets[k], s1 = h_offsets[k + 1];
       if (s0 != h_offsets[next] + pos) tight = false;
-      s.h_off[i - next] = pos;
-      pos += len;
+      pos += s1 > s0 ? s1 - s0 : 0;
     }
-    s.h_off[cnt] = pos;
-    if (h_init) memcpy(s.h_init, h_init + next, cnt * 4);
-    if (tight && pos) tight = host_pinned(src + h_offsets[next], pos);
+    if (tight && bytes) tight = host_pinned(src + h_offsets[next], bytes);
+    // metadata behind the bytes (gathered) or at the buffer's start (tight)
+    const uint64_t meta_off = tight ? 0 : (bytes + 15) / 16 * 16;
+    uint64_t* off = reinterpret_cast<uint64_t*>(s.bulk.h + meta_off);
+    pos = 0;
+    for (uint64_t k = next; k < last; k++) {
+      const uint64_t s0 = h_offsets[k], s1 = h_offsets[k + 1];
+      off[k - next] = pos;
+      pos += s1 > s0 ? s1 - s0 : 0;
+    }
+    off[cnt] = pos;
+    uint32_t* ini = reinterpret_cast<uint32_t*>(off + cnt + 1);
+    if (h_init) memcpy(ini, h_init + next, cnt * 4);
+    const uint64_t meta_n = (cnt + 1) * 8 + (h_init ? cnt * 4 : 0);
+    uint8_t* d_data = s.bulk.d + (tight ? (meta_n + 255) / 256 * 256 : 0);
+    s.settled = false;  // (from here on the stage's stream may hold work)
     if (tight) {
-      e = hipMemcpyAsync(s.d_data, src + h_offsets[next], pos, hipMemcpyHostToDevice, s.stream);
+      e = hipMemcpyAsync(s.bulk.d, s.bulk.h, meta_n, hipMemcpyHostToDevice, s.stream);
+      if (e == hipSuccess && bytes)
+        e = hipMemcpyAsync(d_data, src + h_offsets[next], bytes, hipMemcpyHostToDevice, s.stream);
     } else {
-      gather_blocks(s.h_data, s.h_off, src, h_offsets, next, last);
-      e = hipMemcpyAsync(s.d_data, s.h_data, pos, hipMemcpyHostToDevice, s.stream);
+      // gather over the worker pool: runs of blocks of about equal bytes
+      const uint64_t ways = 2 * ((uint64_t)pool_threads() + 1);
+      const uint64_t per = std::max<uint64_t>(1, (cnt + ways - 1) / ways);
+      parallel_for(bytes < (512u << 10) ? 1 : (size_t)((cnt + per - 1) / per), [&](size_t r) {
+        const uint64_t k0 = next + r * per, k1 = std::min(last, k0 + per);
+        for (uint64_t k = k0; k < k1; k++) {
+          const uint64_t s0 = h_offsets[k], s1 = h_offsets[k + 1];
+          if (s1 > s0) memcpy(s.bulk.h + off[k - next], src + s0, s1 - s0);
+        }
+      });
+      e = hipMemcpyAsync(s.bulk.d, s.bulk.h, meta_off + meta_n, hipMemcpyHostToDevice, s.stream);
     }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess && h_init)
-      e = hipMemcpyAsync(s.d_init, s.h_init, cnt * 4, hipMemcpyHostToDevice, s.stream);
     if (e != hipSuccess) {
       rc = fail_hip(e, "H2D");
       break;
     }
+    uint8_t* d_meta = s.bulk.d + meta_off;
     RaggedArgs a = {};
-    a.base = s.d_data;
-    a.offsets = s.d_off;
+    a.base = d_data;
+    a.offsets = reinterpret_cast<const uint64_t*>(d_meta);
     a.n = cnt;
-    a.init = h_init ? s.d_init : nullptr;
-    a.out = s.d_out;
+    a.init = h_init ? reinterpret_cast<const uint32_t*>(d_meta + (cnt + 1) * 8) : nullptr;
+    a.out = reinterpret_cast<uint32_t*>(s.res.d);
     a.flags = flags;
     a.mode = kModeOut;
     a.dc = st->d_consts;
     a.u_noinit = u_noinit();
     e = launch_ragged(a, (int)st->num_cus, s.stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) {
       rc = fail_hip(e, "staged launch");
       break;
     }
     s.busy = true;
-    s.first = next;
-    s.count = cnt;
+    pend[i] = Pending{next, cnt};
     next = last;
   }
-  for (int k = 0; k < nslots; k++) {
-    int r2 = drain(stg.slot[k]);
+  for (int k = 0; k < HostSession::kStages; k++) {  // (any order: results go to their own slices)
+    const int r2 = drain(k);
     if (rc == LSBM_OK) rc = r2;
   }
-  hipSetDevice(prev);
   return rc;
 }
 
 // Shards one host batch over several devices: contiguous runs of blocks of
-// about equal bytes, one host thread per device, each running the
-// host-staged pipeline above on its own device.  No data moves between the
-// devices (the CRCs are independent); each writes its slice of h_out.
+// about equal bytes, one host thread per device, each bound to its device's
+// NUMA node (its CPUs and its page placement, host_numa.h) and running the
+// host-staged pipeline above on that device, whose staging sits on the same
+// node.  No data moves between the devices (the CRCs are independent); each
+// writes its slice of h_out.
 __attribute__((visibility("default"))) int lsbm_crc32c_batch_host_multi(
     const int* devices, int n_devices, const void* h_base, const uint64_t* h_offsets,
     uint64_t n_blocks, const uint32_t* h_init, uint32_t* h_out, uint32_t flags) {
@@ -895,6 +820,7 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host_multi(
   for (int d = 0; d < n_devices; d++) {
     if (cut[d + 1] <= cut[d]) continue;
     th.emplace_back([&, d] {
+      NumaBind nb(device_numa_node(devices[d]), true, true);
       const uint64_t lo = cut[d], cnt = cut[d + 1] - cut[d];
       rc[d] = lsbm_crc32c_batch_host(devices[d], h_base, h_offsets + lo, cnt,
                                      h_init ? h_init + lo : nullptr, h_out + lo, flags);

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/lsbm_crc32c.h"
+#include "host_numa.h"
 
 namespace lsbm {
 
@@ -49,79 +50,142 @@ bool host_pinned(const void* p, size_t n) {
     const char* b = static_cast<const char*>(base);
     return static_cast<const char*>(p) >= b && last < b + size;
   }
+  // The range cannot be confirmed (hipHostRegister'd memory may not report
+  // one): two registrations with an unregistered gap between them would pass
+  // the first/last-byte test, so take the staging copy.
   (void)hipGetLastError();
-  return true;
+  return false;
 }
 
-// ---- worker pool: one job at a time, the caller works on it too ----
+// ---- worker pool: concurrent jobs, one thread group per NUMA node ----
+//
+// Each job is a piece counter over fn(0) .. fn(pieces - 1).  Jobs from
+// different callers (host layers on different devices, or several sessions
+// of one device) run at the same time: a worker takes the next piece of the
+// oldest job of its own node, else of the oldest job of any node (no idle
+// worker while pieces are left), and the caller works on its own job too.
+// Sized from the CPUs the process may really use (usable_cores(): affinity
+// mask capped by the cgroup quota), split over the nodes in proportion to
+// their CPUs, each worker bound to its node's CPUs when there are several.
 namespace {
 
 // set on the pool's threads, and on a caller while it works on its own job
 thread_local bool t_in_pool = false;
+// the node whose workers a caller's jobs go to first (its session's device)
+thread_local int t_job_node = -1;
+
+struct Job {
+  const std::function<void(size_t)>* fn;
+  size_t pieces, next, finished;
+  int node;
+};
 
 class WorkPool {
  public:
-  void run(size_t pieces, const std::function<void(size_t)>& fn) {
-    std::lock_guard<std::mutex> job(job_mu_);
-    start();
+  void run(size_t pieces, const std::function<void(size_t)>& fn, int node) {
+    Job j{&fn, pieces, 0, 0, node};
     {
       std::lock_guard<std::mutex> l(mu_);
-      fn_ = &fn;
-      pieces_ = pieces;
-      next_ = finished_ = 0;
-      gen_++;
+      start_locked();
+      jobs_.push_back(&j);
+      live_.push_back(&j);
     }
-    cv_.notify_all();
+    if (pieces > 2) work_cv_.notify_all();
+    else work_cv_.notify_one();
     t_in_pool = true;
-    work();
+    for (;;) {  // the caller's share: pieces of its own job only
+      size_t k;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        if (j.next >= j.pieces) break;
+        k = take_locked(&j);
+      }
+      fn(k);
+      std::lock_guard<std::mutex> l(mu_);
+      if (++j.finished == j.pieces) done_cv_.notify_all();
+    }
     t_in_pool = false;
     std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [&] { return finished_ == pieces_; });
-    fn_ = nullptr;
+    done_cv_.wait(l, [&] { return j.finished == j.pieces; });
+    live_.erase(std::find(live_.begin(), live_.end(), &j));
+  }
+  int threads() {
+    std::lock_guard<std::mutex> l(mu_);
+    start_locked();
+    return (int)workers_;
+  }
+  // Testing: the most jobs that had pieces running at once since the last call.
+  int take_peak() {
+    std::lock_guard<std::mutex> l(mu_);
+    const int p = active_max_;
+    active_max_ = 0;
+    return p;
   }
 
  private:
-  void start() {
-    if (!threads_.empty()) return;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    // (the caller is the 16th: the one-GPU box's CPU share is 16)
-    const unsigned nt = std::min(15u, hw > 1 ? hw - 1 : 1u);
-    for (unsigned t = 0; t < nt; t++)
-      threads_.emplace_back([this] {
-        t_in_pool = true;
-        uint64_t seen = 0;
-        for (;;) {
-          {
-            std::unique_lock<std::mutex> l(mu_);
-            cv_.wait(l, [&] { return gen_ != seen; });
-            seen = gen_;
-          }
-          work();
-        }
-      });
-    for (auto& t : threads_) t.detach();  // parked on cv_ for the life of the process
+  // next piece of j (mu_ held); drops j from the queue when it is handed out
+  size_t take_locked(Job* j) {
+    const size_t k = j->next++;
+    if (j->next == j->pieces) jobs_.erase(std::find(jobs_.begin(), jobs_.end(), j));
+    int running = 0;  // jobs with a piece in progress (testing: pool_take_peak_jobs)
+    for (Job* q : live_) running += q->next > q->finished;
+    active_max_ = std::max(active_max_, running);
+    return k;
   }
-  void work() {
-    for (;;) {
-      size_t k;
-      const std::function<void(size_t)>* fn;
-      {
-        std::lock_guard<std::mutex> l(mu_);
-        if (next_ >= pieces_) return;
-        k = next_++;
-        fn = fn_;
+  Job* pick_locked(int node) {
+    for (Job* q : jobs_)
+      if (q->node == node) return q;
+    return jobs_.front();
+  }
+  void start_locked() {
+    if (started_) return;
+    started_ = true;
+    const std::vector<NodeCpus> nodes = process_nodes();
+    const int total = std::max(1, usable_cores() - 1);  // (the caller is the last core)
+    size_t cpus = 0;
+    for (const NodeCpus& n : nodes) cpus += n.cpus.size();
+    const bool bind = nodes.size() > 1;
+    int given = 0;
+    for (size_t i = 0; i < nodes.size(); i++) {
+      // workers in proportion to the node's CPUs (at least one per node)
+      const int left = total - given;
+      int k = i + 1 == nodes.size()
+                  ? left
+                  : std::max(1, (int)((double)total * nodes[i].cpus.size() / std::max<size_t>(1, cpus) + 0.5));
+      k = std::max(0, std::min(k, left));
+      for (int t = 0; t < k; t++) {
+        const int node = nodes[i].node;
+        std::thread th([this, node, bind] { worker(node, bind); });
+        th.detach();  // parked on work_cv_ for the life of the process
       }
-      (*fn)(k);
-      std::lock_guard<std::mutex> l(mu_);
-      if (++finished_ == pieces_) done_cv_.notify_all();
+      given += k;
+      workers_ += k;
     }
   }
-  std::mutex job_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  std::vector<std::thread> threads_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t pieces_ = 0, next_ = 0, finished_ = 0;
-  uint64_t gen_ = 0;
+  void worker(int node, bool bind) {
+    t_in_pool = true;
+    NumaBind nb(bind ? node : -1, true, false);  // (kept bound for the thread's life)
+    for (;;) {
+      Job* j;
+      size_t k;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        work_cv_.wait(l, [&] { return !jobs_.empty(); });
+        j = pick_locked(node);
+        k = take_locked(j);
+      }
+      (*j->fn)(k);
+      std::lock_guard<std::mutex> l(mu_);
+      if (++j->finished == j->pieces) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable work_cv_, done_cv_;
+  std::vector<Job*> jobs_;  // jobs with pieces not yet handed out, oldest first
+  std::vector<Job*> live_;  // jobs not yet collected by their caller
+  size_t workers_ = 0;
+  bool started_ = false;
+  int active_max_ = 0;
 };
 
 WorkPool* pool() {
@@ -130,18 +194,37 @@ WorkPool* pool() {
 }
 
 constexpr int kMaxDevices = 64;
+
+// Sessions of each device: leased one per caller, created on demand up to
+// max_sessions(), kept for reuse (their pinned staging stays allocated).
+struct DeviceSessions {
+  std::vector<HostSession*> all, idle;
+  std::condition_variable cv;
+};
 std::mutex g_reg;
-HostSession* g_sessions[kMaxDevices] = {};
+DeviceSessions g_sessions[kMaxDevices];
+
+int max_sessions() {
+  static const int n = [] {
+    const char* v = getenv("LSBM_HOST_SESSIONS");
+    const int k = v ? atoi(v) : 0;
+    return k > 0 ? std::min(k, 64) : 8;
+  }();
+  return n;
+}
 
 }  // namespace
 
 void parallel_for(size_t pieces, const std::function<void(size_t)>& fn) {
-  if (pieces == 1 || (pieces > 1 && t_in_pool)) {  // (nested: inline, the pool runs one job at a time)
+  if (pieces == 1 || (pieces > 1 && t_in_pool)) {  // (nested: inline on this worker)
     for (size_t k = 0; k < pieces; k++) fn(k);
     return;
   }
-  if (pieces > 1) pool()->run(pieces, fn);
+  if (pieces > 1) pool()->run(pieces, fn, t_job_node);
 }
+
+int pool_threads() { return pool()->threads(); }
+int pool_take_peak_jobs() { return pool()->take_peak(); }
 
 // memcpy into a staging buffer with non-temporal stores: the pinned buffer is
 // only read again by the DMA engine, so its lines need not be read into the
@@ -184,26 +267,39 @@ void stream_copy(char* d, const char* s, size_t n) {
 }
 }  // namespace
 
+// Pieces of about n / (2 (workers + 1)), at least 128 KiB, 4 KiB multiples:
+// every worker gets a share of a 4 MiB chunk (round 3's fixed 1 MiB pieces
+// left 12 of 16 threads idle on one table's 4 MiB chunks: 47 GB/s).
 void parallel_copy(void* dst, const void* src, size_t n) {
-  constexpr size_t kPiece = 1u << 20;
   char* d = static_cast<char*>(dst);
   const char* s = static_cast<const char*>(src);
-  if (n < (4u << 20)) {
+  constexpr size_t kMinPiece = 128u << 10;
+  if (n < 2 * kMinPiece || t_in_pool) {
     stream_copy(d, s, n);
     return;
   }
-  parallel_for((n + kPiece - 1) / kPiece, [&](size_t k) {
-    const size_t off = k * kPiece;
-    stream_copy(d + off, s + off, std::min(kPiece, n - off));
+  const size_t ways = 2 * ((size_t)pool_threads() + 1);
+  const size_t piece = std::max(kMinPiece, ((n + ways - 1) / ways + 4095) / 4096 * 4096);
+  parallel_for((n + piece - 1) / piece, [&](size_t k) {
+    const size_t off = k * piece;
+    stream_copy(d + off, s + off, std::min(piece, n - off));
   });
 }
 
 // ---- buffers ----
+// Page-locked host memory on `node` (the device's NUMA node): the pages are
+// placed by the allocating thread's policy (hipHostMallocNumaUser) set to
+// "prefer node" for the call; without NUMA information, HIP's default.
+static hipError_t host_alloc(void** p, size_t bytes, unsigned flags, int node) {
+  NumaBind nb(node, false, true);
+  return hipHostMalloc(p, bytes, flags | (nb.memory_bound() ? hipHostMallocNumaUser : 0));
+}
+
 hipError_t StagePair::reserve(size_t bytes) {
   if (bytes <= cap && !mapped) return hipSuccess;
   release();
   bytes = std::max<size_t>(bytes, 1u << 16);
-  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault);
+  hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault, node);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), bytes);
   mapped = false;
   if (e != hipSuccess) {
@@ -218,8 +314,7 @@ hipError_t StagePair::reserve_mapped(size_t bytes) {
   if (bytes <= cap && mapped) return hipSuccess;
   release();
   bytes = std::max<size_t>(bytes, 1u << 16);
-  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h), bytes,
-                               hipHostMallocMapped | hipHostMallocCoherent);
+  hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocMapped | hipHostMallocCoherent, node);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
   if (e != hipSuccess) {
     if (h) (void)hipHostFree(h);
@@ -241,7 +336,9 @@ void StagePair::release() {
 
 // ---- session ----
 hipError_t HostSession::init() {
+  node_ = device_numa_node(device_);
   for (Stage& s : stage_) {
+    s.bulk.node = s.meta.node = s.res.node = node_;
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e != hipSuccess) return e;
@@ -283,12 +380,15 @@ hipError_t HostSession::scratch(int k, size_t bytes, void** p) {
 hipError_t HostSession::wait(Stage& s) {
   if (!s.busy) return hipSuccess;
   s.busy = false;
-  return hipEventSynchronize(s.done);
+  const hipError_t e = hipEventSynchronize(s.done);
+  s.settled = e == hipSuccess;
+  return e;
 }
 
 hipError_t HostSession::upload(void* d, const void* h, size_t n) {
   if (n == 0) return hipSuccess;
   Stage& s0 = stage_[0];
+  for (Stage& s : stage_) s.settled = false;
   if (host_pinned(h, n)) {
     hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s0.stream);
     return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
@@ -320,6 +420,7 @@ hipError_t HostSession::upload(void* d, const void* h, size_t n) {
 hipError_t HostSession::download(void* h, const void* d, size_t n) {
   if (n == 0) return hipSuccess;
   Stage& s0 = stage_[0];
+  for (Stage& s : stage_) s.settled = false;
   // (everything the caller enqueued on stage 0's stream comes first)
   if (host_pinned(h, n)) {
     hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s0.stream);
@@ -352,15 +453,13 @@ hipError_t HostSession::download(void* h, const void* d, size_t n) {
 }
 
 void HostSession::ShutdownAll() {
-  std::lock_guard<std::mutex> l(g_reg);
+  std::unique_lock<std::mutex> l(g_reg);
   for (int dev = 0; dev < kMaxDevices; dev++) {
-    HostSession* s = g_sessions[dev];
-    if (!s) continue;
-    {
-      std::lock_guard<std::mutex> sl(s->mu_);  // no lease may be open
-    }
-    delete s;
-    g_sessions[dev] = nullptr;
+    DeviceSessions& ds = g_sessions[dev];
+    ds.cv.wait(l, [&] { return ds.idle.size() == ds.all.size(); });  // no lease may be open
+    for (HostSession* s : ds.all) delete s;
+    ds.all.clear();
+    ds.idle.clear();
   }
 }
 
@@ -371,13 +470,19 @@ void HostSession::ShutdownAll() {
 // index that call's plan) and no DMA from the caller's memory is still in
 // flight when the layer returns.
 SessionLease::~SessionLease() {
-  if (s_)
+  if (s_) {
     for (int i = 0; i < HostSession::kStages; i++) {
       Stage& sg = s_->stage(i);
-      if (sg.stream) (void)hipStreamSynchronize(sg.stream);
+      if (sg.stream && !(sg.settled && !sg.busy)) (void)hipStreamSynchronize(sg.stream);
       sg.busy = false;
+      sg.settled = false;
     }
-  if (lock_.owns_lock()) lock_.unlock();
+    std::lock_guard<std::mutex> l(g_reg);
+    DeviceSessions& ds = g_sessions[s_->device()];
+    ds.idle.push_back(s_);
+    ds.cv.notify_all();
+  }
+  t_job_node = prev_node_;
   delete guard_;
 }
 
@@ -410,28 +515,51 @@ bool host_fault_point(size_t enqueued) {
   return g_fault_after.compare_exchange_strong(n, -1);
 }
 
+// A session of `device` for this caller: an idle one, else a new one while
+// the device has fewer than max_sessions(), else the next one released.
+// Concurrent callers on one device (the reference's writer, compaction and
+// reader threads) each get their own stages and streams and run at once.
 Status SessionLease::Open(int device) {
   if (device < 0 || device >= kMaxDevices) return Status::InvalidArgument("bad device ordinal");
   if (lsbm_crc32c_init(device) != LSBM_OK) return Status::IOError(lsbm_crc32c_last_error());
   guard_ = new DeviceGuard(device);
   if (guard_->status() != hipSuccess) return hip_status(guard_->status(), "hipSetDevice");
   HostSession* s = nullptr;
+  bool fresh = false;
   {
-    std::lock_guard<std::mutex> l(g_reg);
-    s = g_sessions[device];
-    if (!s) {
+    std::unique_lock<std::mutex> l(g_reg);
+    DeviceSessions& ds = g_sessions[device];
+    ds.cv.wait(l, [&] { return !ds.idle.empty() || (int)ds.all.size() < max_sessions(); });
+    if (!ds.idle.empty()) {
+      s = ds.idle.back();
+      ds.idle.pop_back();
+    } else {
       s = new HostSession(device);
-      const hipError_t e = s->init();  // streams on `device` (current)
-      if (e != hipSuccess) {
-        delete s;
-        return hip_status(e, "session streams");
-      }
-      g_sessions[device] = s;
+      ds.all.push_back(s);  // (counted now, so that concurrent opens respect the cap)
+      fresh = true;
     }
   }
-  lock_ = std::unique_lock<std::mutex>(s->mu_);
+  if (fresh) {
+    const hipError_t e = s->init();  // streams on `device` (current)
+    if (e != hipSuccess) {
+      std::lock_guard<std::mutex> l(g_reg);
+      DeviceSessions& ds = g_sessions[device];
+      ds.all.erase(std::find(ds.all.begin(), ds.all.end(), s));
+      delete s;
+      ds.cv.notify_all();
+      return hip_status(e, "session streams");
+    }
+  }
   s_ = s;
+  prev_node_ = t_job_node;
+  t_job_node = s->node();
   return Status::OK();
+}
+
+int session_count(int device) {
+  if (device < 0 || device >= kMaxDevices) return 0;
+  std::lock_guard<std::mutex> l(g_reg);
+  return (int)g_sessions[device].all.size();
 }
 
 }  // namespace lsbm
@@ -441,4 +569,25 @@ Status SessionLease::Open(int device) {
 extern "C" __attribute__((visibility("default"))) int lsbm_test_fail_host_pipeline(int chunks) {
   lsbm::g_fault_after.store(chunks < 0 ? -1 : chunks);
   return 0;
+}
+
+extern "C" __attribute__((visibility("default"))) int lsbm_host_threads(void) {
+  return lsbm::pool_threads();
+}
+
+extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_overlap(int callers, int jobs, int pieces,
+                                                                         int piece_us, double* seconds) {
+  if (callers <= 0 || jobs <= 0 || pieces <= 0 || piece_us < 0) return -1;
+  (void)lsbm::pool_take_peak_jobs();
+  const double t0 = lsbm::HostTiming::now();
+  std::vector<std::thread> th;
+  for (int c = 0; c < callers; c++)
+    th.emplace_back([=] {
+      for (int j = 0; j < jobs; j++)
+        lsbm::parallel_for((size_t)pieces,
+                           [=](size_t) { std::this_thread::sleep_for(std::chrono::microseconds(piece_us)); });
+    });
+  for (auto& t : th) t.join();
+  if (seconds) *seconds = lsbm::HostTiming::now() - t0;
+  return lsbm::pool_take_peak_jobs();
 }

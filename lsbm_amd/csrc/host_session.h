@@ -2,8 +2,10 @@
 // (table_checksum.cc, log_checksum.cc, filter_block.cc, block_compression.cc)
 // and the host-staged batch entry point (crc32c_engine.cc).
 //
-// A HostSession belongs to one device and is created on that device the
-// first time a layer uses it: kStages pipeline stages, each a non-blocking
+// A HostSession belongs to one device and is created on that device when a
+// layer needs one and none is idle (up to LSBM_HOST_SESSIONS, default 8, per
+// device: concurrent callers on one device each lease their own): kStages
+// pipeline stages, each a non-blocking
 // stream, a completion event and three pinned-host / device buffer pairs
 // (bulk bytes, per-item inputs, per-item results) that grow on demand and are
 // kept, plus a few device scratch buffers for single-shot layers.  Nothing is
@@ -13,6 +15,8 @@
 // Copies into pinned memory are the host's share of the work: copies of 4 MiB
 // and more are split over a pool of worker threads so that the staging
 // keeps up with PCIe (~55 GB/s measured for pinned H2D on the MI355X box).
+// The pinned buffers sit on the device's NUMA node (host_numa.h), and the
+// session's copy jobs go to that node's workers first.
 // A source that is already page-locked (hipHostMalloc / hipHostRegister) is
 // DMA-ed directly.  All DMA is stream-ordered hipMemcpyAsync on the stage's
 // stream: a synchronous hipMemcpy from pageable memory may return before its
@@ -61,6 +65,7 @@ struct StagePair {
   uint8_t* d = nullptr;
   size_t cap = 0;
   bool mapped = false;
+  int node = -1;  // NUMA node of the host pages (-1: HIP's default placement)
   hipError_t reserve(size_t bytes);  // grows (never shrinks); contents are not kept
   hipError_t reserve_mapped(size_t bytes);
   void release();
@@ -71,6 +76,12 @@ struct Stage {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   bool busy = false;  // work enqueued whose results the caller has not collected
+  // Within a lease: true only while the stream is known to be idle (the last
+  // thing on it was an event that wait() has seen complete).  A layer clears
+  // it before it enqueues; the lease's release then skips the stream sync of a
+  // settled stage (an idle-stream hipStreamSynchronize is a GPU round trip,
+  // 15-20 us, profiles/r04/one_table).
+  bool settled = false;
   uint64_t tag = 0;   // the caller's chunk number
   StagePair bulk, meta, res;
 };
@@ -78,16 +89,16 @@ struct Stage {
 class HostSession {
  public:
 #ifndef LSBM_HOST_STAGES  // (A/B builds override)
-#define LSBM_HOST_STAGES 3
+#define LSBM_HOST_STAGES 4
 #endif
 #ifndef LSBM_HOST_CHUNK_MB
 #define LSBM_HOST_CHUNK_MB 64
 #endif
   static constexpr int kStages = LSBM_HOST_STAGES;
   static constexpr size_t kChunkBytes = (size_t)LSBM_HOST_CHUNK_MB << 20;  // bulk bytes per stage and chunk (at most)
-  static constexpr size_t kMinChunkBytes = 4u << 20;
+  static constexpr size_t kMinChunkBytes = 2u << 20;
   // Chunk size for a job of `total` bytes: about a quarter of it, so that even
-  // one table's copy, DMA and kernel overlap, within [4 MiB, 64 MiB].
+  // one table's copy, DMA and kernel overlap, within [2 MiB, 64 MiB].
   static size_t chunk_for(size_t total) {
     const size_t q = total / 4;
     return q < kMinChunkBytes ? kMinChunkBytes : (q > kChunkBytes ? kChunkBytes : q);
@@ -97,8 +108,13 @@ class HostSession {
   Stage& stage(int i) { return stage_[i]; }
   // Device scratch buffer k (k < kScratch), at least `bytes` long.
   hipError_t scratch(int k, size_t bytes, void** p);
-  hipStream_t stream() const { return stage_[0].stream; }
+  // Stage 0's stream, for a layer's own enqueues (so no longer settled).
+  hipStream_t stream() {
+    stage_[0].settled = false;
+    return stage_[0].stream;
+  }
   int device() const { return device_; }
+  int node() const { return node_; }
 
   // Host -> device / device -> host of n bytes on stage 0's stream, through
   // the stages' pinned buffers (overlapped) unless `h` is page-locked.
@@ -118,15 +134,17 @@ class HostSession {
   ~HostSession();
   hipError_t init();
   int device_;
-  std::mutex mu_;
+  int node_ = -1;
   Stage stage_[kStages];
   void* scratch_[kScratch] = {};
   size_t scratch_cap_[kScratch] = {};
 };
 
-// The device's session, locked for this caller, with the device current for
-// the lease's lifetime (the caller's current device is restored after).
-// On release every stage is drained and marked idle, whatever the caller left.
+// One of the device's sessions, held by this caller alone, with the device
+// current for the lease's lifetime (the caller's current device is restored
+// after) and the caller's pool jobs steered to the device's NUMA node.  On
+// release every stage is drained and marked idle, whatever the caller left,
+// and the session goes back to the device's idle list.
 class SessionLease {
  public:
   SessionLease() = default;
@@ -141,19 +159,27 @@ class SessionLease {
  private:
   HostSession* s_ = nullptr;
   DeviceGuard* guard_ = nullptr;
-  std::unique_lock<std::mutex> lock_;
+  int prev_node_ = -1;
 };
+
+// Sessions created so far for `device` (idle or leased).
+int session_count(int device);
 
 // Is [p, p + n) inside page-locked host memory (hipHostMalloc'd or registered)?
 bool host_pinned(const void* p, size_t n);
 
-// fn(0) ... fn(pieces - 1) over the worker pool (15 threads and the caller),
-// one job at a time; returns when all have run.  A call from inside a pool
-// task runs its pieces inline on that thread (no deadlock, no extra
-// parallelism).  Concurrent callers (host layers on different devices) take
-// turns for the whole pool: each job is one staging copy or one header pass,
-// about a millisecond, so the turns interleave finely.
+// fn(0) ... fn(pieces - 1) over the worker pool and the caller; returns when
+// all have run.  The pool has usable_cores() - 1 threads (the affinity mask
+// capped by the cgroup CPU quota), grouped by NUMA node; jobs of concurrent
+// callers run at the same time, each worker preferring jobs of its own node
+// (the caller's session's device node).  A call from inside a pool task runs
+// its pieces inline on that thread (no deadlock, no extra parallelism).
 void parallel_for(size_t pieces, const std::function<void(size_t)>& fn);
+
+// The pool's worker count (starts it), and, for tests, the most jobs that
+// had pieces running at the same moment since the previous call.
+int pool_threads();
+int pool_take_peak_jobs();
 
 // memcpy of n bytes, split over the worker pool when n >= 4 MiB.
 void parallel_copy(void* dst, const void* src, size_t n);

@@ -87,6 +87,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
     for (size_t i = 0; i < c.count; i++) hh[i] = heads[c.first + i] - c.lo;
     if (tm.on) tm.add(HostTiming::kPrep, HostTiming::now() - tp);
+    sg.settled = false;  // (from here on the stage's stream may hold work)
     if (pinned) {
       e = hipMemcpyAsync(sg.bulk.d, img + c.lo, bytes, hipMemcpyHostToDevice, sg.stream);
     } else {
@@ -419,6 +420,7 @@ static Status verify_log_streamed(int device, const char* file, uint64_t size, u
     if (e != hipSuccess) return hip_status(e, "staging buffers");
     uint64_t* hh = reinterpret_cast<uint64_t*>(sg.meta.h);
     for (size_t i = 0; i < count; i++) hh[i] = (*heads)[first_h + i] - lo;
+    sg.settled = false;  // (from here on the stage's stream may hold work)
     e = pinned ? hipMemcpyAsync(sg.bulk.d, file + lo, hi - lo, hipMemcpyHostToDevice, sg.stream)
                : hipMemcpyAsync(sg.bulk.d, sg.bulk.h, hi - lo, hipMemcpyHostToDevice, sg.stream);
     if (e == hipSuccess)

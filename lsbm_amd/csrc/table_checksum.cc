@@ -1,12 +1,18 @@
 // table_checksum.cc -- include/lsbm/table_checksum.h on top of the C ABI.
 //
-// The blocks of one or many table images are packed into chunks of at most
-// 64 MiB of whole blocks (with their trailers), and the chunks run through
-// the device's persistent HostSession stages (host_session.h), three deep:
+// The blocks of one or many table images are packed into chunks of whole
+// blocks (with their trailers) of about equal size, at most 64 MiB, and the
+// chunks run through a HostSession's stages (host_session.h), four deep:
 // while chunk c's bytes cross PCIe, chunk c-1 is checksummed and chunk c-2's
 // results come back.  Only 4 B (seal: the masked trailer crc, dense, written
 // into the host image by the host) or 1 B (verify: the ok flag) per block
 // return to the host, never the image.
+//
+// One 16 MiB table per call (TableBuilder::Finish, lsbm/db_impl.cc:843-892)
+// is four 4 MiB chunks, one per stage, so no chunk waits for a stage to come
+// free.  A pageable chunk's handles and types travel in its staging buffer
+// behind its bytes (one DMA per chunk); a page-locked chunk's metadata is
+// sent first, so that its kernel follows its bytes' DMA directly.
 #include "../../include/lsbm/table_checksum.h"
 
 #include <hip/hip_runtime_api.h>
@@ -61,12 +67,16 @@ struct Plan {
 };
 
 // Whole blocks (and trailers) in offset order, packed into chunks of at most
-// HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own).
+// HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own),
+// closed once they reach an equal share of the bytes: no runt chunk at the
+// end (a 1-block fifth chunk cost a kernel launch and a blit per 16 MiB
+// table, profiles/r04/one_table).
 void make_plan(const TableImage* tables, size_t count, Plan* p) {
   p->order.resize(count);
   size_t total = 0;
   for (size_t t = 0; t < count; t++) total += tables[t].file_size;
   const size_t limit = HostSession::chunk_for(total);
+  const size_t target = total / std::max<size_t>(1, (total + limit - 1) / limit);
   Chunk cur;
   auto close = [&]() {
     if (cur.blocks == 0) return;
@@ -93,7 +103,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
       if (open) {
         Piece& pc = cur.pieces.back();
         const uint64_t hi = std::max(pc.hi, end);
-        if (cur.bytes + (hi - pc.hi) <= limit) {
+        if (cur.bytes < target && cur.bytes + (hi - pc.hi) <= limit) {
           cur.bytes += hi - pc.hi;
           pc.hi = hi;
           pc.count++;
@@ -102,7 +112,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
         }
         close();
       }
-      if (cur.blocks && cur.bytes + (end - h.offset) > limit) close();
+      if (cur.blocks && (cur.bytes >= target || cur.bytes + (end - h.offset) > limit)) close();
       cur.pieces.push_back(Piece{(uint32_t)t, h.offset, end, k, 1, cur.bytes});
       cur.bytes += end - h.offset;
       cur.blocks++;
@@ -132,6 +142,10 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
   if (!st.ok()) return st;
   const size_t meta_bytes = plan.max_blocks * (sizeof(BlockHandle) + 1) + 16;
   const size_t res_bytes = plan.max_blocks * 4 + 16;
+  // a pageable chunk's staging: its bytes, then (16-B aligned) its handles and types
+  size_t max_chunk = HostSession::kChunkBytes;
+  for (const Chunk& ch : plan.chunks) max_chunk = std::max<size_t>(max_chunk, ch.bytes);
+  const size_t bulk_bytes = max_chunk + std::max<size_t>(meta_bytes + 16, HostSession::kChunkBytes / 4);
   size_t nbad = 0;
 
   // chunk sg.tag's results, from its stage (host side)
@@ -199,44 +213,50 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
     }
     if (host_fault_point(c)) return Status::IOError("injected fault");  // (tests)
     const Chunk& ch = plan.chunks[c];
-    hipError_t e = sg.bulk.reserve(std::max<size_t>(HostSession::kChunkBytes, ch.bytes));
-    if (e == hipSuccess) e = sg.meta.reserve(meta_bytes);
+    bool direct = true;
+    for (const Piece& pc : ch.pieces) direct = direct && pinned[pc.t];
+    hipError_t e = sg.bulk.reserve(bulk_bytes);
+    if (e == hipSuccess && direct) e = sg.meta.reserve(meta_bytes);
     if (e == hipSuccess) e = sg.res.reserve_mapped(res_bytes);  // (the kernel writes the host buffer)
     if (e != hipSuccess) return hip_status(e, "staging buffers");
     // per-block inputs: handles rebased into the chunk, then the types
-    BlockHandle* hh = reinterpret_cast<BlockHandle*>(sg.meta.h);
-    uint8_t* ty = sg.meta.h + ch.blocks * sizeof(BlockHandle);
+    const size_t meta_off = direct ? 0 : (ch.bytes + 15) / 16 * 16;
+    uint8_t* meta_h = direct ? sg.meta.h : sg.bulk.h + meta_off;
+    uint8_t* meta_d = direct ? sg.meta.d : sg.bulk.d + meta_off;
+    BlockHandle* hh = reinterpret_cast<BlockHandle*>(meta_h);
+    uint8_t* ty = meta_h + ch.blocks * sizeof(BlockHandle);
     size_t j = 0;
-    bool direct = true;
     for (const Piece& pc : ch.pieces) {
       const TableImage& tb = tables[pc.t];
+      const std::vector<size_t>& ord = plan.order[pc.t];
       for (size_t k = pc.first; k < pc.first + pc.count; k++, j++) {
-        const size_t b = plan.order[pc.t][k];
+        const size_t b = ord[k];
         hh[j] = BlockHandle{tb.handles[b].offset - pc.lo + pc.dst, tb.handles[b].size};
         if (op == Op::kSeal) ty[j] = tb.types[b];
       }
-      direct = direct && pinned[pc.t];
     }
-    // the bytes: DMA straight from page-locked images, else via the stage's pinned buffer
+    const size_t meta_n = ch.blocks * sizeof(BlockHandle) + (op == Op::kSeal ? ch.blocks : 0);
+    sg.settled = false;  // (from here on the stage's stream may hold work)
     if (direct) {
+      // page-locked: the metadata first, then the bytes DMA-ed in place
+      e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, sg.stream);
       for (const Piece& pc : ch.pieces)
         if (e == hipSuccess)
           e = hipMemcpyAsync(sg.bulk.d + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo,
                              hipMemcpyHostToDevice, sg.stream);
     } else {
+      // pageable: bytes and metadata through the pinned staging, one DMA
       const double t = tm.on ? HostTiming::now() : 0.0;
       for (const Piece& pc : ch.pieces)
         parallel_copy(sg.bulk.h + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo);
       if (tm.on) tm.add(HostTiming::kCopy, HostTiming::now() - t);
-      e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, ch.bytes, hipMemcpyHostToDevice, sg.stream);
+      e = hipMemcpyAsync(sg.bulk.d, sg.bulk.h, meta_off + meta_n, hipMemcpyHostToDevice, sg.stream);
     }
-    const size_t meta_n = ch.blocks * sizeof(BlockHandle) + (op == Op::kSeal ? ch.blocks : 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, sg.stream);
     if (e != hipSuccess) return hip_status(e, "H2D");
-    const uint64_t* d_h = reinterpret_cast<const uint64_t*>(sg.meta.d);
+    const uint64_t* d_h = reinterpret_cast<const uint64_t*>(meta_d);
     int rc;
     if (op == Op::kSeal)
-      rc = lsbm_sst_trailer_crcs_dev(sg.bulk.d, ch.bytes, d_h, sg.meta.d + ch.blocks * sizeof(BlockHandle),
+      rc = lsbm_sst_trailer_crcs_dev(sg.bulk.d, ch.bytes, d_h, meta_d + ch.blocks * sizeof(BlockHandle),
                                      ch.blocks, reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream);
     else
       rc = lsbm_sst_verify_dev(sg.bulk.d, ch.bytes, d_h, ch.blocks, sg.res.d, nullptr, sg.stream);

@@ -423,6 +423,32 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     assert r.stdout.startswith("OK")
 
 
+@pytest.mark.parametrize("pinned", [0, 1])
+def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned):
+    """4 threads each sealing their own 16 MiB table, one table per call
+    (tests/cpp/concurrent_seal_test.cc): trailers byte-identical to the same
+    calls made one after another and to util/crc32c.h's WriteRawBlock pattern,
+    concurrent verify finds every block good and exactly one flipped block
+    per table, and the concurrent calls take measurably less wall time (each
+    caller leases its own session of the device)."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "concurrent_seal_test"
+    libdir = os.path.join(repo, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(repo, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(repo, "tests", "cpp", "concurrent_seal_test.cc"), "-L", libdir,
+                    "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "4", "8", str(pinned)], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK"), r.stdout
+    speedup = float(r.stdout.split("speedup=")[1].split()[0])
+    assert speedup >= 1.1, r.stdout
+
+
 def test_level2_binding_over_the_reference_table_code(torch_cuda):
     """integration/leveldb_gpu_checksum.h, linked with the reference's own
     table/ and util/ objects (oracle/Makefile gpubind, built in the build
@@ -804,3 +830,49 @@ def test_host_staged_multi_device_shards(torch_cuda, oracle):
     for devs in ([0], [0, 0], [0, 0, 0, 0]):
         got = engine.crc32c_batch_host_multi(data, offs, devs, init=init, masked=True)
         assert np.array_equal(got, oracle.batch_offsets(data, offs, init, masked=True)), devs
+
+
+def test_sst_handles_past_the_image_merged_seal(torch_cuda, oracle):
+    """The same "truncated block read" handles (table/format.cc:88-91) at
+    >= 131,072 blocks, where lsbm_sst_seal_dev computes the CRCs densely and
+    each wave merges its own trailers after its last row: the merge skips
+    handles past the image, writes no byte outside the fitting
+    trailers and leaves the guard bytes after the image alone."""
+    torch = torch_cuda
+    from lsbm_amd import table
+    rng = np.random.default_rng(13)
+    n = 140_000
+    sizes = rng.integers(0, 300, n)
+    handles, total = table.layout_blocks(sizes)
+    handles = handles.astype(np.int64).copy()
+    img = stream_bytes(13, 0, total)
+    guard = np.full(4096, 0xA5, dtype=np.uint8)
+    full = np.concatenate([img, guard])
+    d_full = _dev(torch, full)
+    d = d_full[:total]
+    bad = {5: (total - 2, 0), 70_000: (total + 100, 1), 100_001: (2**62, 10), 139_990: (total - 10, 6),
+           64: (int(handles[2 * 64]), total), n - 1: (total - 4, 0)}
+    orig = {i: (int(handles[2 * i]), int(handles[2 * i + 1])) for i in bad}
+    for i, (o, sz) in bad.items():
+        handles[2 * i], handles[2 * i + 1] = o, sz
+    types = rng.integers(0, 2, n).astype(np.uint8)
+    nbad = table.seal_blocks(d, _dev(torch, handles), _dev(torch, types))
+    assert int(nbad.item()) == len(bad)
+    out = d_full.cpu().numpy()
+    assert np.array_equal(out[total:], guard)
+    good = np.array([i not in bad for i in range(n)])
+    offs, szs = handles[0::2][good], handles[1::2][good]
+    # every fitting trailer: [type][Mask(crc(block || type))]
+    assert np.array_equal(out[offs + szs], types[good])
+    parts = [out[o:o + s + 1] for o, s in zip(offs, szs)]
+    bo = np.zeros(len(parts) + 1, dtype=np.uint64)
+    bo[1:] = np.cumsum([p.size for p in parts])
+    want = oracle.batch_offsets(np.concatenate(parts), bo, masked=True)
+    t = offs + szs
+    stored = (out[t + 1].astype(np.uint32) | (out[t + 2].astype(np.uint32) << 8) |
+              (out[t + 3].astype(np.uint32) << 16) | (out[t + 4].astype(np.uint32) << 24))
+    assert np.array_equal(stored, want)
+    # the bad handles' original trailer slots were never written (their
+    # handles were replaced before the seal)
+    for i, (o, sz) in orig.items():
+        assert np.array_equal(out[o + sz:o + sz + 5], img[o + sz:o + sz + 5]), i

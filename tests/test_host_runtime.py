@@ -1,0 +1,113 @@
+"""CPU checks of the host runtime under the C++ layers (no GPU compute).
+
+* NUMA placement inputs: a GPU's PCI bus id -> <sysfs>/bus/pci/devices/<id>/
+  numa_node (host_numa.cc), cpulist parsing, the cgroup CPU quota (v2 cpu.max
+  and v1 cfs files), all against fake sysfs / cgroup trees;
+* the worker pool: sized from the usable cores (affinity mask capped by the
+  cgroup quota), and jobs of concurrent callers run at the same time instead
+  of taking turns for the whole pool (round 3's pool ran one job at a time).
+
+SURVEY.md 8(e) asks for each GPU's shard to be staged from pinned memory on
+that GPU's NUMA node; the reference's writer, compaction and reader threads
+run concurrently (util/env_posix.cc:546-586, lsbm/db_bench.cc:711-736).
+"""
+import ctypes
+import os
+
+import pytest
+
+
+def _lib(product_lib):
+    from lsbm_amd import _lib
+    return _lib.lib()
+
+
+def test_pci_bus_id_to_numa_node(product_lib, tmp_path):
+    lib = _lib(product_lib)
+    devs = tmp_path / "bus" / "pci" / "devices"
+    for bdf, node in (("0000:0a:00.0", "0\n"), ("0000:8b:00.0", "1\n"), ("0000:c1:00.0", "-1\n"),
+                      ("0000:d9:00.0", "garbage\n")):
+        (devs / bdf).mkdir(parents=True)
+        (devs / bdf / "numa_node").write_text(node)
+    root = str(tmp_path).encode()
+    assert lib.lsbm_test_pci_numa_node(root, b"0000:0a:00.0") == 0
+    assert lib.lsbm_test_pci_numa_node(root, b"0000:8B:00.0") == 1  # (HIP may report upper case)
+    assert lib.lsbm_test_pci_numa_node(root, b"0000:c1:00.0") == -1  # no NUMA information
+    assert lib.lsbm_test_pci_numa_node(root, b"0000:d9:00.0") == -1
+    assert lib.lsbm_test_pci_numa_node(root, b"0000:ff:00.0") == -1  # absent
+    assert lib.lsbm_test_pci_numa_node(root, b"") == -1
+
+
+@pytest.mark.parametrize("text,want", [
+    ("0-3,8,10-11", [0, 1, 2, 3, 8, 10, 11]),
+    ("0-63,128-191\n", list(range(64)) + list(range(128, 192))),
+    ("5", [5]),
+    ("", []),
+    ("\n", []),
+    ("3-1", None),
+    ("a-b", None),
+    ("1,,2", [1, 2]),
+    ("0-", None),
+])
+def test_cpulist_parsing(product_lib, text, want):
+    lib = _lib(product_lib)
+    buf = (ctypes.c_int * 512)()
+    n = lib.lsbm_test_parse_cpulist(text.encode(), buf, 512)
+    if want is None:
+        assert n == -1
+    else:
+        assert n == len(want) and list(buf[:n]) == want
+
+
+def test_cgroup_quota(product_lib, tmp_path):
+    lib = _lib(product_lib)
+    v2 = tmp_path / "v2"
+    v2.mkdir()
+    (v2 / "cpu.max").write_text("1600000 100000\n")  # the GPU box: 16 CPUs
+    assert lib.lsbm_test_cgroup_quota(str(v2).encode()) == 16
+    (v2 / "cpu.max").write_text("max 100000\n")
+    assert lib.lsbm_test_cgroup_quota(str(v2).encode()) == 0
+    (v2 / "cpu.max").write_text("50000 100000\n")  # half a CPU still counts as one
+    assert lib.lsbm_test_cgroup_quota(str(v2).encode()) == 1
+    v1 = tmp_path / "v1" / "cpu"
+    v1.mkdir(parents=True)
+    (v1 / "cpu.cfs_quota_us").write_text("250000\n")
+    (v1 / "cpu.cfs_period_us").write_text("100000\n")
+    assert lib.lsbm_test_cgroup_quota(str(tmp_path / "v1").encode()) == 2
+    (v1 / "cpu.cfs_quota_us").write_text("-1\n")
+    assert lib.lsbm_test_cgroup_quota(str(tmp_path / "v1").encode()) == 0
+    assert lib.lsbm_test_cgroup_quota(str(tmp_path / "none").encode()) == 0
+
+
+def test_pool_sized_from_usable_cores(product_lib):
+    lib = _lib(product_lib)
+    usable = len(os.sched_getaffinity(0))
+    q = lib.lsbm_test_cgroup_quota(None)
+    if q > 0:
+        usable = min(usable, q)
+    if os.environ.get("LSBM_HOST_THREADS"):
+        usable = int(os.environ["LSBM_HOST_THREADS"])
+    assert lib.lsbm_host_threads() == max(1, usable - 1)
+
+
+def test_pool_runs_concurrent_callers_at_once(product_lib):
+    """4 callers x 6 jobs of 2 pieces (3 ms each) against 1 caller x 24 of the
+    same jobs: the pool serves the callers' jobs side by side (at least two
+    jobs have pieces running at the same moment) and the work finishes
+    measurably sooner than one job at a time."""
+    lib = _lib(product_lib)
+    if lib.lsbm_host_threads() < 3:
+        pytest.skip("needs >= 3 pool threads")
+    t_serial, t_conc = ctypes.c_double(), ctypes.c_double()
+    peak1 = lib.lsbm_test_pool_overlap(1, 24, 2, 3000, ctypes.byref(t_serial))
+    peak4 = lib.lsbm_test_pool_overlap(4, 6, 2, 3000, ctypes.byref(t_conc))
+    assert peak1 == 1
+    assert peak4 >= 2
+    assert t_conc.value < 0.8 * t_serial.value, (t_conc.value, t_serial.value)
+
+
+def test_pool_nested_jobs_and_errors(product_lib):
+    lib = _lib(product_lib)
+    assert lib.lsbm_test_pool_overlap(0, 1, 1, 0, None) == -1
+    assert lib.lsbm_test_pool_overlap(2, 3, 1, 0, None) >= 0  # one-piece jobs run inline
+    assert lib.lsbm_test_pool_overlap(8, 4, 64, 50, None) >= 1

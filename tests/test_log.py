@@ -232,3 +232,71 @@ def test_log_seal_and_verify_entry_points(torch_cuda, oracle):
     assert ok.cpu().tolist() == [0, 0, fits] and int(nbad.item()) == 3 - fits
     _, nb2 = log.seal_records(short, tail)
     assert int(nb2.item()) == 3 - fits
+
+
+def _log_crcs_oracle(oracle, img, heads, lens):
+    """Mask(Value(type || payload)) of every record (common/log_writer.cc:85-88):
+    the bytes [h + 6, h + 7 + len) are contiguous in the image."""
+    parts = [img[int(h) + 6:int(h) + 7 + int(n)] for h, n in zip(heads, lens)]
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([p.size for p in parts])
+    buf = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return oracle.batch_offsets(buf, offs, masked=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", [1, 2], ids=["units", "stream"])
+@pytest.mark.parametrize("order", ["in_order", "shuffled"])
+def test_log_seal_deferred_headers_past_the_image(torch_cuda, oracle, policy, order):
+    """lsbm_log_seal_dev with d_masked (the stream kernel defers its header
+    stores to each wave's end) on an image cut inside a record's payload near
+    its end: records that fit get their header CRC written and in out[]; the
+    cut record and every record after it (headers past the image) count as
+    bad, get out[] = 0, and none of their bytes or the guard bytes after the
+    image change.  Shuffled header offsets also send windows through the
+    stream kernel's units fallback (the deferred path's bad-record
+    branch was never run)."""
+    torch = torch_cuda
+    from lsbm_amd import log
+    from lsbm_amd._lib import lib
+    rng = np.random.default_rng(31 + policy)
+    lens = rng.integers(0, 2541, size=12000)
+    lens[-40] = 2000  # the record the cut lands in
+    pay = stream_bytes(0xD1, 0, int(lens.sum()))
+    po = np.concatenate([[0], np.cumsum(lens)])
+    img, heads = log.layout_records(pay[po[i]:po[i + 1]].tobytes() for i in range(lens.size))
+    plen = img[heads + 4].astype(np.int64) | (img[heads + 5].astype(np.int64) << 8)
+    k = int(np.nonzero(plen > 100)[0][-5])  # a physical record near the end with a payload
+    cut = int(heads[k]) + 7 + int(plen[k]) // 2
+    guard = np.full(4096, 0xA5, dtype=np.uint8)
+    full = np.concatenate([img[:cut], guard])
+    before = full.copy()
+    d_full = torch.from_numpy(full).to("cuda")
+    d = d_full[:cut]
+    idx = np.arange(heads.size)
+    if order == "shuffled":
+        rng.shuffle(idx)
+    dh = torch.from_numpy(heads[idx].copy()).to("cuda")
+    lib().lsbm_test_ragged_kernel(policy)
+    try:
+        masked, nbad = log.seal_records(d, dh)
+        torch.cuda.synchronize()
+    finally:
+        lib().lsbm_test_ragged_kernel(0)
+    out = d_full.cpu().numpy()
+    got = masked.cpu().numpy().view(np.uint32)
+    fits = heads[idx] + 7 + plen[idx] <= cut
+    assert int(nbad.item()) == int((~fits).sum()) == heads.size - k
+    assert np.array_equal(out[cut:], guard)
+    want = _log_crcs_oracle(oracle, img, heads[idx][fits], plen[idx][fits])
+    assert np.array_equal(got[fits], want)
+    assert not got[~fits].any()
+    hw = heads[idx][fits]
+    stored = (out[hw].astype(np.uint32) | (out[hw + 1].astype(np.uint32) << 8) |
+              (out[hw + 2].astype(np.uint32) << 16) | (out[hw + 3].astype(np.uint32) << 24))
+    assert np.array_equal(stored, want)
+    # nothing else changed: every byte but the fitting headers' CRC fields
+    written = np.zeros(out.size, dtype=bool)
+    for b in range(4):
+        written[hw + b] = True
+    assert np.array_equal(out[~written], before[~written])

@@ -415,6 +415,24 @@ def wal(args):
     t_seal_sorted = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hsp, n, mp, bp, sp), s)
     nbad.zero_()
     t_ver_sorted = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hsp, n, op, bp, sp), s)
+    sorted_ok = bool(ok.all().item())
+    # every header offset shuffled (no order at all), and both out-of-order
+    # inputs on the units kernel alone (lsbm_test_ragged_kernel(1)) in the same run
+    dhx = torch.from_numpy(heads[np.random.default_rng(0xA3).permutation(n)].astype(heads.dtype)).to("cuda")
+    hxp = ctypes.c_void_p(dhx.data_ptr())
+    t_seal_shuf = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hxp, n, mp, bp, sp), s)
+    t_ver_shuf = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hxp, n, op, bp, sp), s)
+    shuf_ok = bool(ok.all().item())
+    L.lsbm_test_ragged_kernel(1)
+    try:
+        u_seal_sorted = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hsp, n, mp, bp, sp), s)
+        u_ver_sorted = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hsp, n, op, bp, sp), s)
+        u_seal_shuf = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hxp, n, mp, bp, sp), s)
+        u_ver_shuf = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hxp, n, op, bp, sp), s)
+        u_seal = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hp, n, mp, bp, sp), s)
+        u_ver = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hp, n, op, bp, sp), s)
+    finally:
+        L.lsbm_test_ragged_kernel(0)
     o = oracle()
     bad = 0
     for i in range(0, n, max(1, n // 2000)):
@@ -430,7 +448,12 @@ def wal(args):
                                      "all_ok": bool(ok.all().item())},
                       "extents_same_bytes": {"ms": round(t_ext * 1e3, 3), "pct_hbm_peak": pct(t_ext)},
                       "len_sorted_512": {"seal_pct_hbm_peak": pct(t_seal_sorted), "verify_pct_hbm_peak": pct(t_ver_sorted),
-                                         "verify_all_ok": bool(ok.all().item())},
+                                         "verify_all_ok": sorted_ok},
+                      "shuffled": {"seal_pct_hbm_peak": pct(t_seal_shuf), "verify_pct_hbm_peak": pct(t_ver_shuf),
+                                   "verify_all_ok": shuf_ok},
+                      "units_kernel": {"in_order": {"seal": pct(u_seal), "verify": pct(u_ver)},
+                                       "len_sorted_512": {"seal": pct(u_seal_sorted), "verify": pct(u_ver_sorted)},
+                                       "shuffled": {"seal": pct(u_seal_shuf), "verify": pct(u_ver_shuf)}},
                       "sample_mismatches": bad}), flush=True)
 
 

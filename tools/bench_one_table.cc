@@ -1,0 +1,254 @@
+// bench_one_table.cc -- the reference's own call granularity for the table
+// layer: one 16 MiB table per SealBlocks / VerifyBlocks call, as
+// TableBuilder::Finish would make it (lsbm/db_impl.cc:843-892 finishes one
+// output table at a time), timed call by call.
+//
+// Prints one JSON line per phase with the per-call distribution (p50 / p90 /
+// p99 / max / mean, the slowest calls' indices) and the cgroup CPU throttling
+// counters (/sys/fs/cgroup/cpu.stat: nr_periods, nr_throttled,
+// throttled_usec) read before and after the phase:
+//   seal_pageable, verify_pageable        reps calls each, back to back
+//   alternate_pageable                    seal, verify, seal, ... (reps each)
+//   seal_locked, verify_locked            the same image hipHostRegister'ed
+//   concurrent_seal                       C caller threads, each sealing its
+//                                         own table reps / C times, against the
+//                                         same calls made one after another
+//
+//   build: make -C tools bench_one_table
+//   run:   build/bench_one_table [reps=100] [callers=4] [table_mib=16] [idle_ms=0]
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lsbm/table_checksum.h"
+#include "lsbm_crc32c.h"
+#include "util/crc32c.h"
+
+namespace {
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double g_t_first = 0;  // the first layer call of the process (set by main)
+
+uint64_t splitmix(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Table {
+  std::vector<char> img;
+  std::vector<lsbm::BlockHandle> h;
+  std::vector<uint8_t> types;
+};
+
+// db_bench-shaped: 4,118-B data blocks with trailers, printable bytes
+void make_table(Table* t, uint64_t seed, size_t bytes) {
+  const size_t n = bytes / (4118 + lsbm::kBlockTrailerSize);
+  uint64_t fs = 0;
+  t->h = lsbm::LayoutBlocks(std::vector<uint64_t>(n, 4118), &fs);
+  t->img.assign(fs, 0);
+  uint64_t x = seed;
+  for (size_t i = 0; i < fs; i += 8) {
+    uint64_t r = splitmix(x);
+    for (size_t k = 0; k < 8 && i + k < fs; k++, r >>= 8) t->img[i + k] = (char)(' ' + (r & 0xff) % 95);
+  }
+  t->types.assign(n, 0);
+}
+
+int check_table(const Table& t) {
+  int bad = 0;
+  for (size_t i = 0; i < t.h.size(); i++) {
+    const char* b = t.img.data() + t.h[i].offset;
+    const uint32_t crc = leveldb::crc32c::Extend(leveldb::crc32c::Value(b, t.h[i].size), b + t.h[i].size, 1);
+    uint32_t stored;
+    memcpy(&stored, b + t.h[i].size + 1, 4);
+    bad += leveldb::crc32c::Unmask(stored) != crc;
+  }
+  return bad;
+}
+
+struct CpuStat {
+  long long periods = -1, throttled = -1, throttled_us = -1, usage_us = -1;
+};
+CpuStat read_cpu_stat() {
+  CpuStat c;
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return c;
+  char key[64];
+  long long v;
+  while (fscanf(f, "%63s %lld", key, &v) == 2) {
+    if (!strcmp(key, "nr_periods")) c.periods = v;
+    else if (!strcmp(key, "nr_throttled")) c.throttled = v;
+    else if (!strcmp(key, "throttled_usec")) c.throttled_us = v;
+    else if (!strcmp(key, "usage_usec")) c.usage_us = v;
+  }
+  fclose(f);
+  return c;
+}
+
+std::string dist_json(std::vector<double> v, double bytes) {
+  if (v.empty()) return "{}";
+  std::vector<size_t> idx(v.size());
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return v[a] > v[b]; });
+  double mean = 0;
+  for (double x : v) mean += x;
+  mean /= v.size();
+  std::vector<double> s = v;
+  std::sort(s.begin(), s.end());
+  auto q = [&](double p) { return s[std::min(s.size() - 1, (size_t)(p * (s.size() - 1) + 0.5))]; };
+  char buf[1024];
+  std::string slow;
+  for (size_t k = 0; k < std::min<size_t>(5, idx.size()); k++) {
+    char t[64];
+    snprintf(t, sizeof(t), "%s[%zu, %.3f]", k ? ", " : "", idx[k], v[idx[k]] * 1e3);
+    slow += t;
+  }
+  snprintf(buf, sizeof(buf),
+           "{\"calls\": %zu, \"p50_ms\": %.3f, \"p90_ms\": %.3f, \"p99_ms\": %.3f, \"max_ms\": %.3f, "
+           "\"mean_ms\": %.3f, \"min_ms\": %.3f, \"p50_GBps\": %.2f, \"p99_over_p50\": %.2f, \"slowest\": [%s]}",
+           v.size(), q(0.5) * 1e3, q(0.9) * 1e3, q(0.99) * 1e3, s.back() * 1e3, mean * 1e3, s.front() * 1e3,
+           bytes / q(0.5) / 1e9, q(0.99) / q(0.5), slow.c_str());
+  return buf;
+}
+
+void print_phase(const char* what, const std::vector<double>& v, double bytes, const CpuStat& a,
+                 const CpuStat& b, const char* status, int bad, const std::vector<double>& starts = {}) {
+  double slow_at = -1;  // the slowest call's start, ms after the process's first layer call
+  if (!starts.empty())
+    slow_at = (starts[std::max_element(v.begin(), v.end()) - v.begin()] - g_t_first) * 1e3;
+  printf("{\"what\": \"%s\", \"bytes\": %.0f, \"dist\": %s, \"slowest_at_ms\": %.1f, \"cpu_stat\": {\"nr_periods\": %lld, "
+         "\"nr_throttled\": %lld, \"throttled_ms\": %.3f, \"cpu_ms\": %.1f}, \"status\": \"%s\", \"bad\": %d}\n",
+         what, bytes, dist_json(v, bytes).c_str(), slow_at, b.periods - a.periods, b.throttled - a.throttled,
+         (b.throttled_us - a.throttled_us) / 1e3, (b.usage_us - a.usage_us) / 1e3, status, bad);
+  fflush(stdout);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 100;
+  const int callers = argc > 2 ? atoi(argv[2]) : 4;
+  const size_t mib = argc > 3 ? strtoul(argv[3], nullptr, 10) : 16;
+  const int idle_ms = argc > 4 ? atoi(argv[4]) : 0;  // pause after the warm-up calls
+  if (lsbm_crc32c_init(0) != LSBM_OK) {
+    fprintf(stderr, "no device: %s\n", lsbm_crc32c_last_error());
+    return 1;
+  }
+  Table t;
+  make_table(&t, 1, mib << 20);
+  const double bytes = (double)t.img.size();
+  lsbm::Status s;
+  std::vector<uint8_t> ok;
+  // warm: the session's staging for this shape, the pool's threads
+  g_t_first = now();
+  for (int r = 0; r < 3; r++) {
+    s = lsbm::SealBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.types.data(), t.h.size());
+    if (s.ok()) s = lsbm::VerifyBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.h.size(), &ok);
+  }
+  if (!s.ok()) {
+    fprintf(stderr, "warm-up: %s\n", s.ToString().c_str());
+    return 1;
+  }
+  if (idle_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(idle_ms));
+  auto seal = [&](Table& tb) {
+    return lsbm::SealBlocks(0, tb.img.data(), tb.img.size(), tb.h.data(), tb.types.data(), tb.h.size());
+  };
+  auto verify = [&](Table& tb) {
+    return lsbm::VerifyBlocks(0, tb.img.data(), tb.img.size(), tb.h.data(), tb.h.size(), &ok);
+  };
+  auto phase = [&](const char* what, const std::function<lsbm::Status()>& call) {
+    std::vector<double> v, starts;
+    const CpuStat a = read_cpu_stat();
+    lsbm::Status st;
+    for (int r = 0; r < reps && st.ok(); r++) {
+      const double t0 = now();
+      st = call();
+      v.push_back(now() - t0);
+      starts.push_back(t0);
+    }
+    const CpuStat b = read_cpu_stat();
+    print_phase(what, v, bytes, a, b, st.ToString().c_str(), check_table(t), starts);
+    return st.ok();
+  };
+  for (int locked = 0; locked < 2; locked++) {
+    if (locked && hipHostRegister(t.img.data(), t.img.size(), hipHostRegisterDefault) != hipSuccess) {
+      fprintf(stderr, "hipHostRegister failed\n");
+      return 1;
+    }
+    const std::string sfx = locked ? "_locked" : "_pageable";
+    if (!phase(("seal" + sfx).c_str(), [&] { return seal(t); })) return 1;
+    if (!phase(("verify" + sfx).c_str(), [&] { return verify(t); })) return 1;
+    if (!locked) {
+      // seal and verify alternating: is the seal's tail the order it runs in?
+      std::vector<double> vs, vv;
+      const CpuStat a = read_cpu_stat();
+      for (int r = 0; r < reps && s.ok(); r++) {
+        double t0 = now();
+        s = seal(t);
+        vs.push_back(now() - t0);
+        t0 = now();
+        if (s.ok()) s = verify(t);
+        vv.push_back(now() - t0);
+      }
+      const CpuStat b = read_cpu_stat();
+      print_phase("alternate_seal_pageable", vs, bytes, a, b, s.ToString().c_str(), check_table(t));
+      print_phase("alternate_verify_pageable", vv, bytes, a, b, s.ToString().c_str(), 0);
+      if (!s.ok()) return 1;
+    }
+    if (locked) (void)hipHostUnregister(t.img.data());
+  }
+  // concurrent callers, each with its own table, against the same calls in turn
+  if (callers > 1) {
+    std::vector<Table> ts(callers);
+    for (int c = 0; c < callers; c++) make_table(&ts[c], 100 + c, mib << 20);
+    const int per = std::max(1, reps / callers);
+    for (int c = 0; c < callers; c++) (void)seal(ts[c]);
+    const CpuStat a0 = read_cpu_stat();
+    double t0 = now();
+    bool all_ok = true;
+    for (int r = 0; r < per; r++)
+      for (int c = 0; c < callers; c++) all_ok = seal(ts[c]).ok() && all_ok;
+    const double serial = now() - t0;
+    const CpuStat a1 = read_cpu_stat();
+    std::atomic<int> fails{0};
+    std::vector<std::vector<double>> lat(callers);
+    t0 = now();
+    std::vector<std::thread> th;
+    for (int c = 0; c < callers; c++)
+      th.emplace_back([&, c] {
+        for (int r = 0; r < per; r++) {
+          const double u = now();
+          if (!seal(ts[c]).ok()) fails++;
+          lat[c].push_back(now() - u);
+        }
+      });
+    for (auto& x : th) x.join();
+    const double conc = now() - t0;
+    const CpuStat a2 = read_cpu_stat();
+    std::vector<double> all;
+    for (auto& l : lat) all.insert(all.end(), l.begin(), l.end());
+    int bad = 0;
+    for (auto& tb : ts) bad += check_table(tb);
+    printf("{\"what\": \"concurrent_seal\", \"callers\": %d, \"calls_per_caller\": %d, \"bytes_per_call\": %.0f, "
+           "\"serial_s\": %.4f, \"serial_GBps\": %.2f, \"concurrent_s\": %.4f, \"concurrent_GBps\": %.2f, "
+           "\"speedup\": %.3f, \"concurrent_call_dist\": %s, \"serial_throttled\": %lld, "
+           "\"concurrent_throttled\": %lld, \"fails\": %d, \"bad\": %d}\n",
+           callers, per, bytes, serial, callers * per * bytes / serial / 1e9, conc,
+           callers * per * bytes / conc / 1e9, serial / conc, dist_json(all, bytes).c_str(),
+           a1.throttled - a0.throttled, a2.throttled - a1.throttled, fails.load() + (all_ok ? 0 : 1), bad);
+  }
+  return lsbm_crc32c_shutdown() == LSBM_OK ? 0 : 1;
+}
