@@ -46,26 +46,34 @@ inline Status SealTrailersOnGpu(const uint8_t* d_file, uint64_t file_bytes, char
   uint32_t* d_bad = nullptr;
   std::vector<uint32_t> m(n);
   uint32_t nbad = 0;
-  int rc = LSBM_ERR_HIP;
-  if (hipMallocAsync(reinterpret_cast<void**>(&d_h), hh.size() * 8, s) == hipSuccess &&
-      hipMallocAsync(reinterpret_cast<void**>(&d_t), n, s) == hipSuccess &&
-      hipMallocAsync(reinterpret_cast<void**>(&d_m), n * 4, s) == hipSuccess &&
-      hipMallocAsync(reinterpret_cast<void**>(&d_bad), 4, s) == hipSuccess &&
-      hipMemcpyAsync(d_h, hh.data(), hh.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-      hipMemcpyAsync(d_t, types.data(), n, hipMemcpyHostToDevice, s) == hipSuccess &&
-      hipMemsetAsync(d_bad, 0, 4, s) == hipSuccess) {
+  // the first failing HIP call outside the library (its message, not the
+  // library's last error, goes into the Status), or the library's return code
+  hipError_t herr = hipSuccess;
+  int rc = LSBM_OK;
+  auto hip = [&](hipError_t e) {
+    if (e != hipSuccess && herr == hipSuccess) herr = e;
+    return herr == hipSuccess;
+  };
+  if (hip(hipMallocAsync(reinterpret_cast<void**>(&d_h), hh.size() * 8, s)) &&
+      hip(hipMallocAsync(reinterpret_cast<void**>(&d_t), n, s)) &&
+      hip(hipMallocAsync(reinterpret_cast<void**>(&d_m), n * 4, s)) &&
+      hip(hipMallocAsync(reinterpret_cast<void**>(&d_bad), 4, s)) &&
+      hip(hipMemcpyAsync(d_h, hh.data(), hh.size() * 8, hipMemcpyHostToDevice, s)) &&
+      hip(hipMemcpyAsync(d_t, types.data(), n, hipMemcpyHostToDevice, s)) &&
+      hip(hipMemsetAsync(d_bad, 0, 4, s))) {
     rc = lsbm_sst_trailer_crcs_dev(d_file, file_bytes, d_h, d_t, n, d_m, d_bad, s);
-    if (rc == LSBM_OK &&
-        (hipMemcpyAsync(m.data(), d_m, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-         hipMemcpyAsync(&nbad, d_bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess))
-      rc = LSBM_ERR_HIP;
+    if (rc == LSBM_OK) {
+      (void)(hip(hipMemcpyAsync(m.data(), d_m, n * 4, hipMemcpyDeviceToHost, s)) &&
+             hip(hipMemcpyAsync(&nbad, d_bad, 4, hipMemcpyDeviceToHost, s)));
+    }
   }
   if (d_h) (void)hipFreeAsync(d_h, s);
   if (d_t) (void)hipFreeAsync(d_t, s);
   if (d_m) (void)hipFreeAsync(d_m, s);
   if (d_bad) (void)hipFreeAsync(d_bad, s);
-  if (hipStreamSynchronize(s) != hipSuccess && rc == LSBM_OK) rc = LSBM_ERR_HIP;
+  (void)hip(hipStreamSynchronize(s));
   if (rc != LSBM_OK) return Status::IOError("gpu seal", lsbm_crc32c_last_error());
+  if (herr != hipSuccess) return Status::IOError("gpu seal", hipGetErrorString(herr));
   if (nbad) return Status::Corruption("truncated block read");  // a handle past the image
   for (size_t i = 0; i < n; i++) {  // table/table_builder.cc:245-249
     char* t = host_file + h[i].offset() + h[i].size();
@@ -77,17 +85,35 @@ inline Status SealTrailersOnGpu(const uint8_t* d_file, uint64_t file_bytes, char
 
 // ReadBlock's checksum check for n blocks of a device-resident image (handles
 // as {offset, size} pairs in device memory): ok[i] per block, and the status
-// ReadBlock would return for the first bad one.
+// ReadBlock would return for the first bad one -- Corruption("truncated block
+// read") for a handle whose n + 5 bytes leave the image (table/format.cc:88-91),
+// else Corruption("block checksum mismatch") (:95-103).  Only when some block
+// fails are ok[] and the handles copied back, to find that first one.
 inline Status VerifyBlocksOnGpu(const uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles,
                                 uint64_t n, uint8_t* d_ok, uint32_t* d_nbad, hipStream_t s) {
-  if (hipMemsetAsync(d_nbad, 0, 4, s) != hipSuccess) return Status::IOError("gpu verify", "memset");
+  hipError_t e = hipMemsetAsync(d_nbad, 0, 4, s);
+  if (e != hipSuccess) return Status::IOError("gpu verify", hipGetErrorString(e));
   if (lsbm_sst_verify_dev(d_file, file_bytes, d_handles, n, d_ok, d_nbad, s) != LSBM_OK)
     return Status::IOError("gpu verify", lsbm_crc32c_last_error());
   uint32_t nbad = 0;
-  if (hipMemcpyAsync(&nbad, d_nbad, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return Status::IOError("gpu verify", "copy");
-  return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
+  e = hipMemcpyAsync(&nbad, d_nbad, 4, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return Status::IOError("gpu verify", hipGetErrorString(e));
+  if (nbad == 0) return Status::OK();
+  std::vector<uint8_t> ok(n);
+  std::vector<uint64_t> hh(2 * n);
+  e = hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(hh.data(), d_handles, 2 * n * 8, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return Status::IOError("gpu verify", hipGetErrorString(e));
+  for (uint64_t i = 0; i < n; i++) {
+    if (ok[i]) continue;
+    const uint64_t off = hh[2 * i], size = hh[2 * i + 1];
+    const bool truncated = off > file_bytes || size > file_bytes - off ||
+                           file_bytes - off - size < kBlockTrailerSize;
+    return Status::Corruption(truncated ? "truncated block read" : "block checksum mismatch");
+  }
+  return Status::Corruption("block checksum mismatch");
 }
 
 }  // namespace leveldb

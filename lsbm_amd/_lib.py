@@ -59,6 +59,7 @@ SIGNATURES = {
     "lsbm_test_parse_cpulist": (_int, [ctypes.c_char_p, _vp, _int]),
     "lsbm_test_cgroup_quota": (_int, [ctypes.c_char_p]),
     "lsbm_test_pool_overlap": (_int, [_int, _int, _int, _int, _vp]),
+    "lsbm_test_host_pinned": (_int, [_vp, _sz]),
     # include/lsbm_bloom.h
     "lsbm_bloom_hash": (_u32, [_vp, _sz, _u32]),
     "lsbm_bloom_filter_bytes": (_u64, [_u64, _int]),

@@ -3,6 +3,16 @@
 #pragma once
 #include <stdint.h>
 
+// Diagnostic A/B macros that make a build compute wrong results on purpose
+// (results not stored, stored CRCs rewritten, bloom probes not set) are
+// refused unless the build also says it is a diagnostic one: such a library
+// is only ever written under build/ab/ (tools/build_variant.sh), never the
+// product lsbm_amd/liblsbm_crc32c.so.
+#if (defined(LSBM_DIAG_NO_STORE) || defined(LSBM_DIAG_VERIFY_WRITEBACK) || \
+     defined(LSBM_DIAG_NO_PROBE_WRITES)) && !defined(LSBM_DIAG_BUILD)
+#error "LSBM_DIAG_* result-changing macros need LSBM_DIAG_BUILD (A/B variant builds only)"
+#endif
+
 namespace lsbm {
 
 constexpr int kBloomThreads = 256;                 // 4 waves per workgroup

@@ -13,11 +13,13 @@
 //     into registers (one per lane) and checks: ascending and non-overlapping
 //     (s_j >= e_{j-1}), within a 2 GiB window; a sub-piece ends before the
 //     first block that is not.  When that leaves fewer than 16 blocks (blocks
-//     out of order) the units walk (any order, any overlap) takes that window
-//     of 63 blocks, and a block that alone spans 2 GiB goes the same way; the
-//     stream resumes after it (round 3 redid the wave's whole range instead,
-//     and out-of-order headers ran at 33% of HBM peak against the units
-//     kernel's 43-54%);
+//     out of order), or a block alone spans 2 GiB, the units walk (any order,
+//     any size), inlined after the stream loop, takes the rest of the wave's
+//     range from that block on.  (Round 3 called it out of line and redid the
+//     wave's whole range: out-of-order headers ran at 33% of HBM peak against
+//     the units kernel's 43-54%; the out-of-line walk spills in its rounds.
+//     Round 4's first try, the out-of-line walk per 63-block window, ran at
+//     26-30%.)
 //   * the sub-piece's rows [floor(s_first / 128), last row] are cut into 8
 //     segments of Q rows, one per lane group, and every group streams its
 //     segment row after row with the fixed kernel's access pattern: one 16-B
@@ -113,22 +115,6 @@ __device__ __forceinline__ uint32_t end_row(uint32_t s, uint32_t e) {
   return e > s ? (e - 1u) >> 7 : s >> 7;
 }
 
-// A block of 2 GiB or more, or a window of blocks out of order: the units
-// walk over blocks [b_lo, b_hi), out of line (its registers are not the
-// stream loop's).  It takes the kernel's argument block from the kernarg
-// segment and the range as two scalars: the argument block passed by value
-// would make the kernel copy it to scratch at its entry, every wave, whether
-// or not it falls back (~13 MB of writes per launch).
-template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
-__device__ __attribute__((noinline)) void units_fallback(const RaggedArgs* __restrict__ ka, uint64_t b_lo,
-                                                         uint64_t b_hi) {
-  const RaggedArgs args = *ka;
-  const uint64_t wave = (uint64_t)blockIdx.x * kStreamWavesPerWg +
-                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * kStreamWavesPerWg;
-  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, false, 0u, 0u, false);
-}
-
 template <uint32_t kR, uint32_t kMode, uint32_t kExt>
 __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArgs args) {
   static_assert(kR % 8 == 0 && kR <= 32, "rows per step: banks of 4");
@@ -165,10 +151,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-  // some window went through the units walk (wave-uniform): its records' fit
-  // is not in nbad, so the deferred-header epilogue re-reads their lengths
-  bool walked = false;
-  const RaggedArgs* ka = (const RaggedArgs*)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  // the first block the stream leaves to the units walk (~0: none; wave-uniform)
+  uint64_t resume = ~0ull;
   // The next sub-piece's extents are loaded while this one streams (its log
   // record lengths, loads that depend on them, behind its first rows): a
   // sub-piece starts without waiting for them.
@@ -258,15 +242,10 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         // The first block alone spans >= 2 GiB (nb == 0), or blocks out of
         // order (e.g. log headers passed by length, shuffled offsets): a
         // sub-piece of a few blocks would cost its setup and tail per block, so
-        // the units walk (any order, any size) takes this window, and the
-        // stream resumes after it.
+        // the units walk takes the rest of the wave's range from b0 on.
         if (nb == 0u || (nb < kSubBlocks / 4u && nb < navail)) {
-          const uint32_t take = nb == 0u ? 1u : navail;
-          units_fallback<kFallbackRows, kMode, kExt>(ka, b0, b0 + take);
-          walked = true;
-          b0 += take;
-          pre = false;
-          continue;
+          resume = b0;
+          break;
         }
         pb = P.pb;
         desc = P.desc;
@@ -668,7 +647,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       LSBM_TOC(5);
       b0 += nb;
     }
-    if (!chunked) break;
+    if (!chunked || resume != ~0ull) break;
     pi += (uint32_t)nwaves;
     if (pi >= p_end) break;
     b_lo = bnd[pi];
@@ -681,6 +660,12 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       atomicAdd(&g_stream_stats[8 + i], (unsigned long long)tm[i]);
     }
 #endif
+  if (resume != ~0ull) {
+    // The units walk from block `resume` on: the rest of this range, then (a
+    // chunked sweep) this wave's range of every later chunk.  Its bad blocks
+    // are counted by the walk; this wave's nbad holds the streamed ones.
+    units_walk<kFallbackRows, kMode, kExt>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end, false, resume);
+  }
   if constexpr (kMode == kModeLogSeal) {
     // Deferred headers: this wave's masked CRCs went densely to out[] with
     // its reads; the scattered header stores follow its last row, so they do
@@ -694,7 +679,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
         ExtRaw r = load_ext_raw(args, i);
         uint64_t at = base + r.x;
         bool fits = true;
-        if (nbad != 0u || walked) {  // (only a wave that may hold a record that does not fit reads the lengths again)
+        if (nbad != 0u || resume != ~0ull) {  // (only a wave that may hold a record that does not fit reads the lengths again)
           log_length(args, r);
           uint64_t s, e;
           extent_from_raw(args, i, r, s, e, fits, at);

@@ -373,10 +373,15 @@ __device__ __forceinline__ void wave_range(const RaggedArgs& args, uint64_t wave
 // every chunk) in rounds of 8 units.  crc32c_units_kernel runs it over the
 // wave's range; crc32c_stream_kernel runs it over a sub-piece whose extents
 // are not in order (load_tables false: the LDS tables are in place).
+//
+// first_lo: the walk starts at block first_lo (>= the range's start) of its
+// first range; the stream kernel resumes there after streaming the blocks
+// before it (chunked too: later ranges are walked whole).
 template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
 __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave, const uint64_t nwaves,
                                            uint64_t b_lo, uint64_t b_hi, const bool chunked,
-                                           uint32_t pi, const uint32_t p_end, const bool load_tables) {
+                                           uint32_t pi, const uint32_t p_end, const bool load_tables,
+                                           const uint64_t first_lo = 0) {
   args.mode = kMode;   // compile-time: lets the compiler drop the other modes' code
   args.extents = kExt;
   const DevConsts* __restrict__ dc = args.dc;
@@ -395,6 +400,7 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
   };
   if (chunked) {
     piece(pi, b_lo, b_hi);
+    b_lo = b_lo < first_lo ? first_lo : b_lo;
     while (b_lo >= b_hi && pi + nwaves < p_end) piece(pi += (uint32_t)nwaves, b_lo, b_hi);  // (empty)
 #ifndef LSBM_NO_BOUNDS_PREFETCH
     if (pi + nwaves < p_end) piece(pi + (uint32_t)nwaves, pf_lo, pf_hi);

@@ -50,9 +50,15 @@ bool host_pinned(const void* p, size_t n) {
     const char* b = static_cast<const char*>(base);
     return static_cast<const char*>(p) >= b && last < b + size;
   }
-  // The range cannot be confirmed (hipHostRegister'd memory may not report
-  // one): two registrations with an unregistered gap between them would pass
-  // the first/last-byte test, so take the staging copy.
+  (void)hipGetLastError();
+  // hipHostRegister'd memory reports no address range: the first and last
+  // bytes must then belong to the same registration (one buffer id), so that
+  // two registrations with an unregistered gap between them do not pass.
+  // Unconfirmed: take the staging copy.
+  unsigned long long id0 = 0, id1 = 0;
+  if (hipPointerGetAttribute(&id0, HIP_POINTER_ATTRIBUTE_BUFFER_ID, const_cast<void*>(p)) == hipSuccess &&
+      hipPointerGetAttribute(&id1, HIP_POINTER_ATTRIBUTE_BUFFER_ID, const_cast<char*>(last)) == hipSuccess)
+    return id0 != 0 && id0 == id1;
   (void)hipGetLastError();
   return false;
 }
@@ -89,6 +95,7 @@ class WorkPool {
       start_locked();
       jobs_.push_back(&j);
       live_.push_back(&j);
+      queued_.store(jobs_.size(), std::memory_order_release);
     }
     if (pieces > 2) work_cv_.notify_all();
     else work_cv_.notify_one();
@@ -126,7 +133,10 @@ class WorkPool {
   // next piece of j (mu_ held); drops j from the queue when it is handed out
   size_t take_locked(Job* j) {
     const size_t k = j->next++;
-    if (j->next == j->pieces) jobs_.erase(std::find(jobs_.begin(), jobs_.end(), j));
+    if (j->next == j->pieces) {
+      jobs_.erase(std::find(jobs_.begin(), jobs_.end(), j));
+      queued_.store(jobs_.size(), std::memory_order_release);
+    }
     int running = 0;  // jobs with a piece in progress (testing: pool_take_peak_jobs)
     for (Job* q : live_) running += q->next > q->finished;
     active_max_ = std::max(active_max_, running);
@@ -162,12 +172,32 @@ class WorkPool {
       workers_ += k;
     }
   }
+  // A worker that runs out of pieces spins for spin_us() before it sleeps on
+  // work_cv_: a layer's chunks come every ~80 us, and a worker woken from
+  // sleep joins a 4 MiB staging copy late (the copy ran at ~51 GB/s on 16
+  // threads, profiles/r04/check3/timing.log).
+  static double spin_us() {
+    static const double us = [] {
+      const char* v = getenv("LSBM_POOL_SPIN_US");
+      return v ? atof(v) : 100.0;
+    }();
+    return us;
+  }
   void worker(int node, bool bind) {
     t_in_pool = true;
     NumaBind nb(bind ? node : -1, true, false);  // (kept bound for the thread's life)
     for (;;) {
       Job* j;
       size_t k;
+      if (queued_.load(std::memory_order_acquire) == 0 && spin_us() > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 1; queued_.load(std::memory_order_acquire) == 0; i++) {
+          _mm_pause();
+          if ((i & 255u) == 0 &&
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us())
+            break;
+        }
+      }
       {
         std::unique_lock<std::mutex> l(mu_);
         work_cv_.wait(l, [&] { return !jobs_.empty(); });
@@ -183,6 +213,7 @@ class WorkPool {
   std::condition_variable work_cv_, done_cv_;
   std::vector<Job*> jobs_;  // jobs with pieces not yet handed out, oldest first
   std::vector<Job*> live_;  // jobs not yet collected by their caller
+  std::atomic<size_t> queued_{0};  // jobs_.size(), for the workers' spin
   size_t workers_ = 0;
   bool started_ = false;
   int active_max_ = 0;
@@ -295,10 +326,20 @@ static hipError_t host_alloc(void** p, size_t bytes, unsigned flags, int node) {
   return hipHostMalloc(p, bytes, flags | (nb.memory_bound() ? hipHostMallocNumaUser : 0));
 }
 
+// A buffer grows to the size asked for plus a quarter (1 MiB granules), so
+// that a session sized by one table's 4 MiB chunks pins ~5 MiB per stage, not
+// a compaction's 80 MiB (a new session pinned 4 x 80 MiB: ~0.3 s), and grows
+// once when larger jobs come.
+static size_t with_headroom(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 1u << 16);
+  if (bytes < (1u << 20)) return bytes;
+  return (bytes + bytes / 4 + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+}
+
 hipError_t StagePair::reserve(size_t bytes) {
   if (bytes <= cap && !mapped) return hipSuccess;
   release();
-  bytes = std::max<size_t>(bytes, 1u << 16);
+  bytes = with_headroom(bytes);
   hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault, node);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), bytes);
   mapped = false;
@@ -313,7 +354,7 @@ hipError_t StagePair::reserve(size_t bytes) {
 hipError_t StagePair::reserve_mapped(size_t bytes) {
   if (bytes <= cap && mapped) return hipSuccess;
   release();
-  bytes = std::max<size_t>(bytes, 1u << 16);
+  bytes = with_headroom(bytes);
   hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocMapped | hipHostMallocCoherent, node);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
   if (e != hipSuccess) {
@@ -590,4 +631,9 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_overlap(int
   for (auto& t : th) t.join();
   if (seconds) *seconds = lsbm::HostTiming::now() - t0;
   return lsbm::pool_take_peak_jobs();
+}
+
+// Testing: host_pinned() itself (which ranges the layers DMA in place).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_host_pinned(const void* p, size_t n) {
+  return lsbm::host_pinned(p, n) ? 1 : 0;
 }

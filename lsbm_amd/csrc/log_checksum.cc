@@ -79,7 +79,7 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     if (host_fault_point(k)) return Status::IOError("injected fault");  // (tests)
     const Chunk& c = chunks[k];
     const uint64_t bytes = c.hi - c.lo;
-    hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
+    hipError_t e = sg.bulk.reserve(kLogChunk);
     if (e == hipSuccess) e = sg.meta.reserve(max_count * sizeof(uint64_t));
     if (e == hipSuccess) e = sg.res.reserve_mapped(max_count * per);  // (the kernel writes the host buffer)
     if (e != hipSuccess) return hip_status(e, "staging buffers");
@@ -394,7 +394,7 @@ static Status verify_log_streamed(int device, const char* file, uint64_t size, u
       if (!st.ok()) return st;
     }
     if (host_fault_point(k)) return Status::IOError("injected fault");  // (tests)
-    hipError_t e = sg.bulk.reserve(HostSession::kChunkBytes);
+    hipError_t e = sg.bulk.reserve(kWin);
     if (e != hipSuccess) return hip_status(e, "staging buffers");
     // copy (unless page-locked) and walk, piece by piece
     const size_t np = (size_t)((hi - lo + kPiece - 1) / kPiece);

@@ -143,9 +143,9 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
   const size_t meta_bytes = plan.max_blocks * (sizeof(BlockHandle) + 1) + 16;
   const size_t res_bytes = plan.max_blocks * 4 + 16;
   // a pageable chunk's staging: its bytes, then (16-B aligned) its handles and types
-  size_t max_chunk = HostSession::kChunkBytes;
+  size_t max_chunk = 0;
   for (const Chunk& ch : plan.chunks) max_chunk = std::max<size_t>(max_chunk, ch.bytes);
-  const size_t bulk_bytes = max_chunk + std::max<size_t>(meta_bytes + 16, HostSession::kChunkBytes / 4);
+  const size_t bulk_bytes = max_chunk + meta_bytes + 32;
   size_t nbad = 0;
 
   // chunk sg.tag's results, from its stage (host side)
@@ -164,10 +164,12 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
     const Chunk& ch = plan.chunks[sg.tag];
     if (op == Op::kSeal) {
       // [type][EncodeFixed32(masked crc)] (table_builder.cc:245-249): scattered
-      // 5-byte stores into the caller's images, split over the worker pool in
-      // runs of kRun blocks (on the pipeline's critical path: ~0.15 ms per
-      // 64 MiB chunk on one thread)
-      constexpr size_t kRun = 2048;
+      // 5-byte stores into the caller's images (each its own page for 4 KiB
+      // blocks: a TLB miss and a line fill per trailer), split over the worker
+      // pool in runs of kRun blocks.  On the pipeline's critical path: ~0.15 ms
+      // per 64 MiB chunk on one thread; with 2,048-block runs a 16 MiB table's
+      // four chunks took ~54 us on one thread each (profiles/r04/check3).
+      constexpr size_t kRun = 256;
       struct Run {
         const Piece* pc;
         size_t k0, k1, j0;

@@ -132,6 +132,20 @@ int main() {
   std::vector<uint8_t> ok(n);
   EXPECT(hipMemcpy(ok.data(), d_ok, n, hipMemcpyDeviceToHost) == hipSuccess);
   for (size_t i = 0; i < n; i++) EXPECT(ok[i] == (i == bad ? 0 : 1));
+  // a handle whose trailer leaves the image, before the flipped block: ReadBlock's
+  // "truncated block read" (table/format.cc:88-91) is the first failure
+  const size_t cut = 1;
+  hh[2 * cut + 1] = sealed.size() - h[cut].offset() - 3;
+  EXPECT(hipMemcpy(d_h, hh.data(), hh.size() * 8, hipMemcpyHostToDevice) == hipSuccess);
+  st = VerifyBlocksOnGpu(d_file, sealed.size(), d_h, n, d_ok, d_nbad, s);
+  BlockHandle th;
+  th.set_offset(hh[2 * cut]);
+  th.set_size(hh[2 * cut + 1]);
+  BlockContents tc;
+  const Status ts = ReadBlock(&file, ro, th, &tc);
+  EXPECT(st.IsCorruption() && ts.IsCorruption());
+  EXPECT(st.ToString() == ts.ToString());
+  EXPECT(st.ToString() == "Corruption: truncated block read");
   (void)hipFree(d_h);
   (void)hipFree(d_ok);
   (void)hipFree(d_nbad);

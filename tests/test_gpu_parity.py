@@ -876,3 +876,38 @@ def test_sst_handles_past_the_image_merged_seal(torch_cuda, oracle):
     # handles were replaced before the seal)
     for i, (o, sz) in orig.items():
         assert np.array_equal(out[o + sz:o + sz + 5], img[o + sz:o + sz + 5]), i
+
+
+def test_host_pinned_ranges(torch_cuda):
+    """Which host ranges the C++ layers DMA in place (host_session.cc
+    host_pinned): a hipHostMalloc'd buffer and one hipHostRegister'd range
+    (which reports no address range, so its buffer id decides) in whole and
+    in part; not a range running past the registration, not two adjacent
+    registrations with a gap, not pageable memory."""
+    import ctypes
+    torch = torch_cuda
+    from lsbm_amd._lib import lib
+    L = lib()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    pinned = torch.empty(3 << 20, dtype=torch.uint8, pin_memory=True)
+    p = pinned.data_ptr()
+    assert L.lsbm_test_host_pinned(p, 3 << 20) == 1
+    assert L.lsbm_test_host_pinned(p + 12345, 1 << 20) == 1
+    page = 4096
+    raw = np.zeros(6 << 20, dtype=np.uint8)
+    a = (raw.ctypes.data + page - 1) // page * page
+    assert L.lsbm_test_host_pinned(a, 1 << 20) == 0  # pageable
+    assert hip.hipHostRegister(a, 2 << 20, 0) == 0
+    try:
+        assert hip.hipHostRegister(a + (2 << 20) + page, 2 << 20, 0) == 0
+        try:
+            assert L.lsbm_test_host_pinned(a, 2 << 20) == 1
+            assert L.lsbm_test_host_pinned(a + 777, (1 << 20) + 5) == 1
+            assert L.lsbm_test_host_pinned(a, (2 << 20) + 1) == 0  # past the registration
+            assert L.lsbm_test_host_pinned(a, (4 << 20) + page) == 0  # two registrations, a gap
+        finally:
+            hip.hipHostUnregister(a + (2 << 20) + page)
+    finally:
+        hip.hipHostUnregister(a)

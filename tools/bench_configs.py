@@ -431,6 +431,10 @@ def wal(args):
         u_ver_shuf = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hxp, n, op, bp, sp), s)
         u_seal = time_launches(lambda: L.lsbm_log_seal_dev(dp, nb, hp, n, mp, bp, sp), s)
         u_ver = time_launches(lambda: L.lsbm_log_verify_dev(dp, nb, hp, n, op, bp, sp), s)
+        # (diagnostic) the stream kernel over the same bytes as {offset, length}
+        # extents: no record-length loads at all (the bound for deriving lengths)
+        L.lsbm_test_ragged_kernel(2)
+        t_ext_stream = time_launches(lambda: L.lsbm_crc32c_extents_dev(dp, ep, n, None, mp, 0, sp), s)
     finally:
         L.lsbm_test_ragged_kernel(0)
     o = oracle()
@@ -446,7 +450,8 @@ def wal(args):
                       "log_crcs": {"ms": round(t_crcs * 1e3, 3), "pct_hbm_peak": pct(t_crcs)},
                       "log_verify": {"ms": round(t_ver * 1e3, 3), "pct_hbm_peak": pct(t_ver),
                                      "all_ok": bool(ok.all().item())},
-                      "extents_same_bytes": {"ms": round(t_ext * 1e3, 3), "pct_hbm_peak": pct(t_ext)},
+                      "extents_same_bytes": {"ms": round(t_ext * 1e3, 3), "pct_hbm_peak": pct(t_ext),
+                                             "stream_kernel_pct_hbm_peak": pct(t_ext_stream)},
                       "len_sorted_512": {"seal_pct_hbm_peak": pct(t_seal_sorted), "verify_pct_hbm_peak": pct(t_ver_sorted),
                                          "verify_all_ok": sorted_ok},
                       "shuffled": {"seal_pct_hbm_peak": pct(t_seal_shuf), "verify_pct_hbm_peak": pct(t_ver_shuf),
