@@ -236,21 +236,35 @@ __device__ __forceinline__ uint32_t fastmod(uint32_t n, uint64_t M, uint32_t d) 
 
 // The probe positions of util/bloom.cc:57-61 / :83-87 are h_j mod d with
 // h_{j+1} = h_j + delta (mod 2^32).  So after the first one,
-//   h_{j+1} mod d = (h_j mod d + delta mod d - wrap_j * (2^32 mod d)) mod d,
-// wrap_j = carry out of h_j + delta: two remainders per key instead of k,
-// then one add, one compare and a rare correction per probe.  Needs d < 2^31.
+//   h_{j+1} mod d = (h_j mod d + s) mod d,
+// s = delta mod d, or (delta - 2^32) mod d when h_j + delta carries out of 32
+// bits: two remainders per key instead of k, then per probe the add with
+// its carry, a select of the step, and p + s reduced as min(p, p - d)
+// (unsigned: p - d wraps when p < d).  Needs d < 2^31.  (Round 3 applied the
+// carry's correction as a second conditional step: 13 VALU per build probe,
+// its LDS address included, against 10 now.)
 struct ProbeSeq {
-  uint32_t pos, dm, c32, d, h, delta;
+  uint32_t pos, d, h, delta, s0, s1;
   __device__ __forceinline__ void next() {
     const uint32_t hn = h + delta;
-    const bool wrap = hn < h;
+    const uint32_t step = hn < h ? s1 : s0;
     h = hn;
-    uint32_t p = pos + dm;
-    if (p >= d) p -= d;
-    if (wrap) p = p >= c32 ? p - c32 : p + (d - c32);
-    pos = p;
+    const uint32_t p = pos + step;
+    pos = min(p, p - d);
   }
 };
+// hm = h mod d, dm = delta mod d, c32 = 2^32 mod d
+__device__ __forceinline__ ProbeSeq probe_seq(uint32_t h, uint32_t delta, uint32_t hm, uint32_t dm,
+                                              uint32_t c32, uint32_t d) {
+  ProbeSeq p;
+  p.pos = hm;
+  p.d = d;
+  p.h = h;
+  p.delta = delta;
+  p.s0 = dm;
+  p.s1 = dm >= c32 ? dm - c32 : dm + (d - c32);
+  return p;
+}
 
 // Orders one wave's LDS phases (its own ds ops complete in order; this keeps
 // the compiler from moving accesses across the phase boundary).
@@ -623,7 +637,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
       const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
       if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
-      ProbeSeq ps{fastmod(h, M, d), fastmod(delta, M, d), c32, d, h, delta};
+      ProbeSeq ps = probe_seq(h, delta, fastmod(h, M, d), fastmod(delta, M, d), c32, d);
 #ifdef LSBM_PROBE_UNROLL  // A/B builds only
 #pragma unroll LSBM_PROBE_UNROLL
 #endif
@@ -683,12 +697,10 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
   const BitMod m = bit_mod(bits);
   const uint32_t delta = (h >> 17) | (h << 15);
   const bool inc = bits < (1ull << 31);  // ProbeSeq's range; else a remainder per probe
-  ProbeSeq ps{0, 0, 0, (uint32_t)bits, h, delta};
+  ProbeSeq ps{0, 0, h, delta, 0, 0};
   if (inc) {
-    ps.pos = mod_bits(h, m);
-    ps.dm = mod_bits(delta, m);
     const uint32_t c = mod_bits(0xffffffffu, m) + 1;  // 2^32 mod bits
-    ps.c32 = c == ps.d ? 0 : c;
+    ps = probe_seq(h, delta, mod_bits(h, m), mod_bits(delta, m), c == (uint32_t)bits ? 0u : c, (uint32_t)bits);
   }
   // The reference stops at the first clear bit (:85); the answer is the same
   // if a chunk of up to 16 probe bytes (all inside this filter) is requested
