@@ -253,6 +253,23 @@ struct ProbeSeq {
     pos = min(p, p - d);
   }
 };
+// The lookup side's form (key_may_match, an out-of-line call per query): the
+// carry's correction applied after the step, which needs no second step
+// register -- the probe kernel's caller then keeps its live registers across
+// the call (with the selected-step form it spilled 16 B per lane per query:
+// 0.49 -> 0.55 ms, profiles/r04/check5/bench_bloom.log).
+struct ProbeSeqLookup {
+  uint32_t pos, dm, c32, d, h, delta;
+  __device__ __forceinline__ void next() {
+    const uint32_t hn = h + delta;
+    const bool wrap = hn < h;
+    h = hn;
+    uint32_t p = pos + dm;
+    if (p >= d) p -= d;
+    if (wrap) p = p >= c32 ? p - c32 : p + (d - c32);
+    pos = p;
+  }
+};
 // hm = h mod d, dm = delta mod d, c32 = 2^32 mod d
 __device__ __forceinline__ ProbeSeq probe_seq(uint32_t h, uint32_t delta, uint32_t hm, uint32_t dm,
                                               uint32_t c32, uint32_t d) {
@@ -697,10 +714,12 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
   const BitMod m = bit_mod(bits);
   const uint32_t delta = (h >> 17) | (h << 15);
   const bool inc = bits < (1ull << 31);  // ProbeSeq's range; else a remainder per probe
-  ProbeSeq ps{0, 0, h, delta, 0, 0};
+  ProbeSeqLookup ps{0, 0, 0, (uint32_t)bits, h, delta};
   if (inc) {
+    ps.pos = mod_bits(h, m);
+    ps.dm = mod_bits(delta, m);
     const uint32_t c = mod_bits(0xffffffffu, m) + 1;  // 2^32 mod bits
-    ps = probe_seq(h, delta, mod_bits(h, m), mod_bits(delta, m), c == (uint32_t)bits ? 0u : c, (uint32_t)bits);
+    ps.c32 = c == ps.d ? 0 : c;
   }
   // The reference stops at the first clear bit (:85); the answer is the same
   // if a chunk of up to 16 probe bytes (all inside this filter) is requested

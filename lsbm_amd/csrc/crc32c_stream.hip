@@ -675,11 +675,13 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     if ((args.flags & kFlagDeferHeaders) && args.file) {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's out[] stores performed
       typedef __attribute__((address_space(1), aligned(1))) uint32_t* gu32u;
-      for (uint64_t i = b_lo + lane; i < b_hi; i += 64u) {
+      // (the units walk wrote the headers of [resume, b_hi) in place)
+      const uint64_t d_hi = resume < b_hi ? resume : b_hi;
+      for (uint64_t i = b_lo + lane; i < d_hi; i += 64u) {
         ExtRaw r = load_ext_raw(args, i);
         uint64_t at = base + r.x;
         bool fits = true;
-        if (nbad != 0u || resume != ~0ull) {  // (only a wave that may hold a record that does not fit reads the lengths again)
+        if (nbad != 0u) {  // (only a wave with a record that does not fit reads the lengths again)
           log_length(args, r);
           uint64_t s, e;
           extent_from_raw(args, i, r, s, e, fits, at);

@@ -166,10 +166,12 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
       // [type][EncodeFixed32(masked crc)] (table_builder.cc:245-249): scattered
       // 5-byte stores into the caller's images (each its own page for 4 KiB
       // blocks: a TLB miss and a line fill per trailer), split over the worker
-      // pool in runs of kRun blocks.  On the pipeline's critical path: ~0.15 ms
-      // per 64 MiB chunk on one thread; with 2,048-block runs a 16 MiB table's
-      // four chunks took ~54 us on one thread each (profiles/r04/check3).
-      constexpr size_t kRun = 256;
+      // pool in runs of kRun blocks: ~0.15 ms per 64 MiB chunk on one thread.
+      // A one-table chunk (~1,000 blocks) is one run, on this thread: 256-block
+      // runs over the pool took 0.10-0.14 ms per 16 MiB table against ~0.05 ms
+      // inline (profiles/r04/check5/timing.log).  The drain below posts each
+      // chunk as soon as its stage completes, under the later chunks' DMA.
+      constexpr size_t kRun = 2048;
       struct Run {
         const Piece* pc;
         size_t k0, k1, j0;

@@ -208,7 +208,52 @@ int main(int argc, char** argv) {
       print_phase("alternate_verify_pageable", vv, bytes, a, b, s.ToString().c_str(), 0);
       if (!s.ok()) return 1;
     }
-    if (locked) (void)hipHostUnregister(t.img.data());
+    if (locked) {
+      // Zero-copy experiment: the device ABI's kernels reading the registered
+      // image over PCIe directly (no DMA, no staging), handles and results in
+      // device memory: is a kernel's own PCIe read stream faster per table
+      // than DMA + kernel?
+      void* dimg = nullptr;
+      uint64_t* dh = nullptr;
+      uint8_t *dt = nullptr, *dok = nullptr;
+      uint32_t* dm = nullptr;
+      hipStream_t st = nullptr;
+      std::vector<uint64_t> hh(2 * t.h.size());
+      for (size_t i = 0; i < t.h.size(); i++) hh[2 * i] = t.h[i].offset, hh[2 * i + 1] = t.h[i].size;
+      bool ok_setup = hipHostGetDevicePointer(&dimg, t.img.data(), 0) == hipSuccess &&
+                      hipMalloc(reinterpret_cast<void**>(&dh), hh.size() * 8) == hipSuccess &&
+                      hipMalloc(reinterpret_cast<void**>(&dt), t.h.size()) == hipSuccess &&
+                      hipMalloc(reinterpret_cast<void**>(&dok), t.h.size()) == hipSuccess &&
+                      hipMalloc(reinterpret_cast<void**>(&dm), t.h.size() * 4) == hipSuccess &&
+                      hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+                      hipMemcpy(dh, hh.data(), hh.size() * 8, hipMemcpyHostToDevice) == hipSuccess &&
+                      hipMemcpy(dt, t.types.data(), t.h.size(), hipMemcpyHostToDevice) == hipSuccess;
+      if (ok_setup) {
+        auto zc = [&](bool seal_mode) {
+          const int rc = seal_mode ? lsbm_sst_trailer_crcs_dev(static_cast<const uint8_t*>(dimg), t.img.size(), dh,
+                                                               dt, t.h.size(), dm, nullptr, st)
+                                   : lsbm_sst_verify_dev(static_cast<const uint8_t*>(dimg), t.img.size(), dh,
+                                                         t.h.size(), dok, nullptr, st);
+          const bool good = rc == LSBM_OK && hipStreamSynchronize(st) == hipSuccess;
+          return good ? lsbm::Status::OK() : lsbm::Status::IOError("zero-copy launch");
+        };
+        for (int w = 0; w < 3; w++) (void)zc(false);
+        if (!phase("zerocopy_trailer_crcs_locked", [&] { return zc(true); })) return 1;
+        if (!phase("zerocopy_verify_locked", [&] { return zc(false); })) return 1;
+        std::vector<uint8_t> okh(t.h.size());
+        (void)hipMemcpy(okh.data(), dok, okh.size(), hipMemcpyDeviceToHost);
+        printf("{\"what\": \"zerocopy_check\", \"blocks_ok\": %zu, \"blocks\": %zu}\n",
+               (size_t)std::count(okh.begin(), okh.end(), 1), okh.size());
+      } else {
+        printf("{\"what\": \"zerocopy\", \"status\": \"setup failed\"}\n");
+      }
+      if (st) (void)hipStreamDestroy(st);
+      (void)hipFree(dh);
+      (void)hipFree(dt);
+      (void)hipFree(dok);
+      (void)hipFree(dm);
+      (void)hipHostUnregister(t.img.data());
+    }
   }
   // concurrent callers, each with its own table, against the same calls in turn
   if (callers > 1) {
