@@ -379,7 +379,7 @@ void StagePair::release() {
 hipError_t HostSession::init() {
   node_ = device_numa_node(device_);
   for (Stage& s : stage_) {
-    s.bulk.node = s.meta.node = s.res.node = node_;
+    s.bulk.node = s.meta.node = s.res.node = s.zmeta.node = node_;
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e != hipSuccess) return e;
@@ -394,6 +394,7 @@ HostSession::~HostSession() {
     s.bulk.release();
     s.meta.release();
     s.res.release();
+    s.zmeta.release();
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }

@@ -84,6 +84,7 @@ struct Stage {
   bool settled = false;
   uint64_t tag = 0;   // the caller's chunk number
   StagePair bulk, meta, res;
+  StagePair zmeta;  // mapped: per-block inputs the kernel reads in place (zero-copy table jobs)
 };
 
 class HostSession {

@@ -430,7 +430,11 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned):
     calls made one after another and to util/crc32c.h's WriteRawBlock pattern,
     concurrent verify finds every block good and exactly one flipped block
     per table, and the concurrent calls take measurably less wall time (each
-    caller leases its own session of the device)."""
+    caller leases its own session of the device) -- pageable images, where one
+    caller's host copy leaves PCIe idle part of the time.  Page-locked images
+    are DMA-ed in place: one caller alone already runs near the PCIe ceiling
+    (~45 of ~52 GB/s, profiles/r04/), so there concurrency must only not
+    cost anything."""
     import os
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -446,7 +450,7 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK"), r.stdout
     speedup = float(r.stdout.split("speedup=")[1].split()[0])
-    assert speedup >= 1.1, r.stdout
+    assert speedup >= (1.1 if pinned == 0 else 0.95), r.stdout
 
 
 def test_level2_binding_over_the_reference_table_code(torch_cuda):

@@ -294,6 +294,10 @@ def main():
         ln["roofline"]["traffic"] = int(t) if t else None
         if t:
             ln["roofline"]["traffic_over_algorithmic"] = round(t / ln["algorithmic_bytes"], 3)
+            # FETCH_SIZE x 2 is the fetched line bytes for every access width on
+            # gfx950, these scattered reads included (tools/fetch_calib.hip:
+            # one memory request per 128-B line, profiles/r04/fetch_calib/)
+            ln["roofline"]["traffic_calibration"] = "profiles/r04/fetch_calib/summary.json"
         if cpu:
             ln["cpu_baseline"] = cpu
         print(json.dumps(ln), flush=True)

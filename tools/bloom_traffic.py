@@ -4,9 +4,11 @@ PMC passes -> profiles/bloom_traffic.json (read by tools/bench_bloom.py).
 
 Reads: FETCH_SIZE (KiB) x 1024 x 2, the gfx950 correction of
 MI355X_MICROARCH.md "HBM" (FETCH_SIZE reports half the bytes of a wide
-coalesced stream; the key stream is one; the probes' 4-B filter reads are not
-calibrated, so the raw x1 figure is kept beside it).  Writes: WRITE_SIZE (KiB)
-x 1024, exact for streaming stores."""
+coalesced stream).  Round 4 calibrated the probes' scattered 1-4 B reads on a
+known line count (tools/fetch_calib.hip, profiles/r04/fetch_calib/): every
+width goes to memory as one request per 128-B line, tallied at 64 B, so the
+same x2 gives their fetched line bytes; the raw x1 figure is kept beside it.
+Writes: WRITE_SIZE (KiB) x 1024, exact for streaming stores."""
 import collections
 import csv
 import glob
