@@ -228,6 +228,10 @@ int lsbm_test_pool_overlap(int callers, int jobs, int pieces, int piece_us, doub
 /* Testing: 1 if the C++ layers would DMA [p, p + n) in place (page-locked by
  * hipHostMalloc or one hipHostRegister covering the whole range), else 0. */
 int lsbm_test_host_pinned(const void* p, size_t n);
+/* Testing: page-locked table jobs up to `mb` MiB are read by the kernel in
+ * place (zero copy) instead of DMA-ed in chunks (LSBM_ZERO_COPY_MAX_MB sets it
+ * at start-up; 0 = never); returns -1 for mb < 0. */
+int lsbm_test_zero_copy_max_mb(int mb);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -382,6 +382,7 @@ hipError_t HostSession::init() {
     s.bulk.node = s.meta.node = s.res.node = s.zmeta.node = node_;
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -389,6 +390,7 @@ hipError_t HostSession::init() {
 
 HostSession::~HostSession() {
   DeviceGuard g(device_);
+  if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
   for (Stage& s : stage_) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     s.bulk.release();
@@ -396,8 +398,10 @@ HostSession::~HostSession() {
     s.res.release();
     s.zmeta.release();
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   for (int k = 0; k < kScratch; k++)
     if (scratch_[k]) (void)hipFree(scratch_[k]);
 }
@@ -416,6 +420,19 @@ hipError_t HostSession::scratch(int k, size_t bytes, void** p) {
     scratch_cap_[k] = cap;
   }
   *p = scratch_[k];
+  return hipSuccess;
+}
+
+hipError_t HostSession::copy_stream(hipStream_t* out) {
+  if (!copy_stream_) {
+    const hipError_t e = hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      copy_stream_ = nullptr;
+      return e;
+    }
+  }
+  copy_pending_ = true;
+  *out = copy_stream_;
   return hipSuccess;
 }
 
@@ -513,12 +530,19 @@ void HostSession::ShutdownAll() {
 // flight when the layer returns.
 SessionLease::~SessionLease() {
   if (s_) {
+    bool all_settled = true;
     for (int i = 0; i < HostSession::kStages; i++) {
       Stage& sg = s_->stage(i);
+      all_settled = all_settled && sg.settled && !sg.busy;
       if (sg.stream && !(sg.settled && !sg.busy)) (void)hipStreamSynchronize(sg.stream);
       sg.busy = false;
       sg.settled = false;
     }
+    // The copy stream's DMAs all precede a stage's kernel (stream-wait on the
+    // stage's `copied` event), so settled stages mean finished copies; on an
+    // error path one may still be reading the caller's memory.
+    if (s_->copy_stream_ && s_->copy_pending_ && !all_settled) (void)hipStreamSynchronize(s_->copy_stream_);
+    s_->copy_pending_ = false;
     std::lock_guard<std::mutex> l(g_reg);
     DeviceSessions& ds = g_sessions[s_->device()];
     ds.idle.push_back(s_);

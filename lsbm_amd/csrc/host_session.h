@@ -75,12 +75,13 @@ struct StagePair {
 struct Stage {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  hipEvent_t copied = nullptr;  // this stage's DMA on the session's copy stream has landed
   bool busy = false;  // work enqueued whose results the caller has not collected
   // Within a lease: true only while the stream is known to be idle (the last
   // thing on it was an event that wait() has seen complete).  A layer clears
   // it before it enqueues; the lease's release then skips the stream sync of a
   // settled stage (an idle-stream hipStreamSynchronize is a GPU round trip,
-  // 15-20 us, profiles/r04/one_table).
+  // 15-20 us, profiles/r04/one_table_trace/summary_call40.txt).
   bool settled = false;
   uint64_t tag = 0;   // the caller's chunk number
   StagePair bulk, meta, res;
@@ -126,6 +127,13 @@ class HostSession {
   // Waits for a stage's enqueued work (no-op if idle); clears busy.
   hipError_t wait(Stage& s);
 
+  // The session's copy stream (created on first use): page-locked chunks'
+  // DMAs all go through it, so they land one after another at the full link
+  // rate and chunk c's kernel (on its stage's stream, after the stage's
+  // `copied` event) runs under chunk c+1's DMA.  On four stage streams the
+  // four DMAs of a table ran side by side and all landed at the end.
+  hipError_t copy_stream(hipStream_t* out);
+
   // Frees every session (lsbm_crc32c_shutdown).
   static void ShutdownAll();
 
@@ -137,6 +145,8 @@ class HostSession {
   int device_;
   int node_ = -1;
   Stage stage_[kStages];
+  hipStream_t copy_stream_ = nullptr;
+  bool copy_pending_ = false;  // copies enqueued during the current lease
   void* scratch_[kScratch] = {};
   size_t scratch_cap_[kScratch] = {};
 };

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <numeric>
 
 #include "../../include/lsbm_crc32c.h"
@@ -71,7 +72,7 @@ struct Plan {
 // HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own),
 // closed once they reach an equal share of the bytes: no runt chunk at the
 // end (a 1-block fifth chunk cost a kernel launch and a blit per 16 MiB
-// table, profiles/r04/one_table).
+// table, profiles/r04/one_table_trace/summary_call40.txt).
 void make_plan(const TableImage* tables, size_t count, Plan* p) {
   p->order.resize(count);
   size_t total = 0;
@@ -127,12 +128,16 @@ enum class Op { kSeal, kVerify };
 
 // Page-locked jobs up to this many bytes (LSBM_ZERO_COPY_MAX_MB, default 64;
 // 0 = never) are read by the kernel in place, see run_zero_copy.
+std::atomic<long> g_zero_copy_mb{-1};  // -1: not read yet
 size_t zero_copy_max() {
-  static const size_t v = [] {
+  long v = g_zero_copy_mb.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("LSBM_ZERO_COPY_MAX_MB");
-    return (size_t)(e ? atol(e) : 64) << 20;
-  }();
-  return v;
+    v = e ? std::max(0L, atol(e)) : 64;
+    long expect = -1;
+    if (!g_zero_copy_mb.compare_exchange_strong(expect, v)) v = expect;
+  }
+  return (size_t)v << 20;
 }
 
 // A small page-locked job -- one table per call, as TableBuilder::Finish
@@ -359,12 +364,18 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
     const size_t meta_n = ch.blocks * sizeof(BlockHandle) + (op == Op::kSeal ? ch.blocks : 0);
     sg.settled = false;  // (from here on the stage's stream may hold work)
     if (direct) {
-      // page-locked: the metadata first, then the bytes DMA-ed in place
-      e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, sg.stream);
+      // page-locked: the metadata first, then the bytes DMA-ed in place, on
+      // the session's copy stream (the chunks' DMAs back to back); the stage's
+      // kernel waits for this chunk's
+      hipStream_t cs = nullptr;
+      e = s->copy_stream(&cs);
+      if (e == hipSuccess) e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, cs);
       for (const Piece& pc : ch.pieces)
         if (e == hipSuccess)
           e = hipMemcpyAsync(sg.bulk.d + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo,
-                             hipMemcpyHostToDevice, sg.stream);
+                             hipMemcpyHostToDevice, cs);
+      if (e == hipSuccess) e = hipEventRecord(sg.copied, cs);
+      if (e == hipSuccess) e = hipStreamWaitEvent(sg.stream, sg.copied, 0);
     } else {
       // pageable: bytes and metadata through the pinned staging, one DMA
       const double t = tm.on ? HostTiming::now() : 0.0;
@@ -449,3 +460,10 @@ Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockH
 }
 
 }  // namespace lsbm
+
+// Testing (include/lsbm_crc32c.h): the zero-copy threshold in MiB (0: never).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_zero_copy_max_mb(int mb) {
+  if (mb < 0) return -1;
+  lsbm::g_zero_copy_mb.store(mb);
+  return 0;
+}

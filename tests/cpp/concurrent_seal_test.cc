@@ -10,7 +10,7 @@
 // calls take measurably less wall time than the serial ones (each caller
 // leases its own session: stages, streams and pinned staging).
 //
-//   concurrent_seal_test [callers=4] [reps=8] [pinned=0]
+//   concurrent_seal_test [callers=4] [reps=8] [pinned=0] [zero_copy_max_mb=64]
 // prints "OK serial_ms=... concurrent_ms=... speedup=..." or FAIL lines.
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
@@ -86,6 +86,9 @@ int main(int argc, char** argv) {
   const int callers = argc > 1 ? atoi(argv[1]) : 4;
   const int reps = argc > 2 ? atoi(argv[2]) : 8;
   const bool pinned = argc > 3 && atoi(argv[3]) != 0;
+  // page-locked one-table jobs: read in place by the kernel (the default) or,
+  // with 0, DMA-ed in chunks through the session's copy stream
+  if (argc > 4) lsbm_test_zero_copy_max_mb(atoi(argv[4]));
   if (lsbm_crc32c_init(0) != LSBM_OK) {
     printf("FAIL no device: %s\n", lsbm_crc32c_last_error());
     return 1;

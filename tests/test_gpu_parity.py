@@ -423,8 +423,9 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     assert r.stdout.startswith("OK")
 
 
-@pytest.mark.parametrize("pinned", [0, 1])
-def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned):
+@pytest.mark.parametrize("pinned,zero_copy_mb", [(0, 64), (1, 64), (1, 0)],
+                         ids=["pageable", "locked-zero-copy", "locked-dma"])
+def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb):
     """4 threads each sealing their own 16 MiB table, one table per call
     (tests/cpp/concurrent_seal_test.cc): trailers byte-identical to the same
     calls made one after another and to util/crc32c.h's WriteRawBlock pattern,
@@ -445,7 +446,8 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned):
                     os.path.join(repo, "tests", "cpp", "concurrent_seal_test.cc"), "-L", libdir,
                     "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
                     "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
-    r = subprocess.run([str(exe), "4", "8", str(pinned)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([str(exe), "4", "8", str(pinned), str(zero_copy_mb)], capture_output=True, text=True,
+                       timeout=120)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK"), r.stdout
