@@ -608,14 +608,17 @@ void bloom_build_kernel(BloomBuildArgs a) {
       const uint32_t r = r0 + lane;
       const bool act = r < nkeys;
       // the last filter of the group whose first key is <= r (empty filters
-      // share their successor's first key and are passed over)
-      uint32_t pos = 1;  // (filter 0 starts at key 0)
-#pragma unroll
-      for (uint32_t step = kBloomGroup / 2; step; step >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)st_t, (int)(pos + step - 1));
-        if (v <= r) pos += step;
-      }
-      const uint32_t j = pos - 1;
+      // share their successor's first key and are passed over): the filters
+      // starting before the round (a ballot), plus those starting inside it at
+      // or before r -- a wave-uniform handful (~2 of 33-key filters per
+      // 64-key round), each read with readlane.  (Round 3: a 5-step binary
+      // search, a chain of dependent ds_bpermute round trips every round.)
+      const uint32_t c0 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0));
+      const uint32_t c1 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0 + 64u));
+      uint32_t cnt = c0;
+      for (uint32_t q = c0; q < c1; q++)
+        cnt += (uint32_t)__builtin_amdgcn_readlane((int)st_t, (int)q) <= r ? 1u : 0u;
+      const uint32_t j = cnt - 1u;  // (filter 0 starts at key 0: cnt >= 1)
       const uint4 sl = slots[wv][j];
       const uint32_t bbase = sl.x, d = sl.y;
       const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;

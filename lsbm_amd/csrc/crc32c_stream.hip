@@ -235,7 +235,19 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
           rq = nx;
         } else {
           rq = load_ext_raw(args, lane < navail ? b0 + lane : b0);
-          if constexpr (kExt == kExtLogHeaders) log_length(args, rq);
+          if constexpr (kExt == kExtLogHeaders) {
+            // Headers out of order already by their offsets (fewer than 16
+            // ascending from b0): the units walk, without waiting for the
+            // record lengths, a load that depends on these.
+            const uint64_t prev = shfl_up64(rq.x, 1);
+            const uint64_t down = __ballot(lane > 0u && lane < navail && rq.x <= prev);
+            const uint32_t asc = down ? (uint32_t)__builtin_ctzll(down) : 64u;
+            if (asc < kSubBlocks / 4u && asc < navail) {
+              resume = b0;
+              break;
+            }
+            log_length(args, rq);
+          }
         }
         const Plan P = plan(b0, navail, rq);
         nb = P.nb;
