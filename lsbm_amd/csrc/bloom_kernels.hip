@@ -784,6 +784,9 @@ constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 3
 #ifndef LSBM_PROBE_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_WAVES_PER_EU 6
 #endif
+#ifndef LSBM_PROBE_HANDLE_AHEAD  // (A/B builds override)
+#define LSBM_PROBE_HANDLE_AHEAD 0
+#endif
 #ifndef LSBM_PROBE_BLOCK_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_BLOCK_WAVES_PER_EU 1
 #endif
@@ -817,17 +820,40 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     plan = plan_span(kbase + oa0, n, avail, safe);
     fetch_span(plan, ch0, ch1);
   }
+#if LSBM_PROBE_HANDLE_AHEAD
+  // the filter handle (and data offset) one round ahead too: a round's probe
+  // loads then wait only for its hash, not for a handle load behind it
+  uint64_t hc, hs, hd = 0;
+  {
+    const uint64_t qq = q00 + lane < a.n ? q00 + lane : 0;
+    hc = a.handles[2 * qq];
+    hs = a.handles[2 * qq + 1];
+    if (a.mode != kProbeFilter) hd = a.data_offsets[qq];
+  }
+#endif
   for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
     const uint64_t ks = kbase + oa0;
     const uint64_t kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+#if LSBM_PROBE_HANDLE_AHEAD
+    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + hc;
+    const uint64_t size = hs;
+    const uint64_t doff = hd;
+    {
+      const uint64_t qn = q + stride < a.n ? q + stride : 0;
+      hc = a.handles[2 * qn];
+      hs = a.handles[2 * qn + 1];
+      if (a.mode != kProbeFilter) hd = a.data_offsets[qn];
+    }
+#else
     // the filter handle (and data offset) do not depend on the hash: requested
     // before it (the hash's LDS fences would otherwise hold them back)
     const uint64_t qq = act ? q : 0;
     const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
     const uint64_t size = a.handles[2 * qq + 1];
     const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
+#endif
     // this round's chunks go to LDS; the next round's plan and loads go out
     const SpanPlan cur = plan;
     const u32x4 cc0 = ch0, cc1 = ch1;

@@ -409,11 +409,9 @@ __attribute__((visibility("default"))) int lsbm_crc32c_verify_dev(
   return run_ragged(a, static_cast<hipStream_t>(stream));
 }
 
-__attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes,
-                                                             const uint64_t* d_handles,
-                                                             const uint8_t* d_types,
-                                                             uint64_t n_blocks, uint32_t* d_nbad,
-                                                             void* stream) {
+// lsbm_sst_seal_dev; in_place: one pass, trailers as plain byte stores
+static int sst_seal_impl(uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles, const uint8_t* d_types,
+             uint64_t n_blocks, uint32_t* d_nbad, void* stream, bool in_place) {
   if (n_blocks == 0) return LSBM_OK;
   if (!d_file || !d_handles || !d_types) return fail(LSBM_ERR_INVALID, "null pointer");
   DeviceState* st = nullptr;
@@ -447,7 +445,7 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
     const char* e = getenv("LSBM_SEAL_MIN_BLOCKS");
     return e ? strtoull(e, nullptr, 10) : (1ull << 17);
   }();
-  if (one_pass || capturing || n_blocks < min_blocks ||
+  if (in_place || one_pass || capturing || n_blocks < min_blocks ||
       hipMallocAsync(reinterpret_cast<void**>(&crcs), n_blocks * sizeof(uint32_t), s) != hipSuccess) {
     (void)hipGetLastError();
     a.file = d_file;
@@ -469,6 +467,14 @@ __attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, ui
   }
   (void)hipFreeAsync(crcs, s);
   return rc;
+}
+
+__attribute__((visibility("default"))) int lsbm_sst_seal_dev(uint8_t* d_file, uint64_t file_bytes,
+                                                             const uint64_t* d_handles,
+                                                             const uint8_t* d_types,
+                                                             uint64_t n_blocks, uint32_t* d_nbad,
+                                                             void* stream) {
+  return sst_seal_impl(d_file, file_bytes, d_handles, d_types, n_blocks, d_nbad, stream, false);
 }
 
 __attribute__((visibility("default"))) int lsbm_sst_trailer_crcs_dev(
@@ -839,3 +845,10 @@ __attribute__((visibility("default"))) int lsbm_test_ragged_kernel(int which) {
 }
 
 }  // extern "C"
+
+namespace lsbm {
+int sst_seal_in_place(uint8_t* d_file, uint64_t file_bytes, const uint64_t* d_handles, const uint8_t* d_types,
+                      uint64_t n_blocks, hipStream_t stream) {
+  return sst_seal_impl(d_file, file_bytes, d_handles, d_types, n_blocks, nullptr, stream, true);
+}
+}  // namespace lsbm

@@ -24,6 +24,7 @@
 #include <numeric>
 
 #include "../../include/lsbm_crc32c.h"
+#include "engine_internal.h"
 #include "host_session.h"
 
 namespace lsbm {
@@ -168,13 +169,23 @@ bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op o
     dev[t] = static_cast<const uint8_t*>(p);
   }
   size_t nbad = 0;
+  // The seal writes its trailers into the image itself, over PCIe (each wave
+  // its own blocks' 5 bytes, posted writes): no host pass over the table's
+  // trailer pages after the kernel.  LSBM_ZERO_COPY_SEAL_POST=1 (A/B): dense
+  // CRCs into a mapped buffer, posted by this thread.
+  static const bool post_on_host = [] {
+    const char* e = getenv("LSBM_ZERO_COPY_SEAL_POST");
+    return e && atoi(e) != 0;
+  }();
   auto collect = [&](Stage& sg) -> Status {
     double t0 = tm.on ? HostTiming::now() : 0.0;
     const hipError_t e = hs.wait(sg);
     if (tm.on) tm.add(HostTiming::kWait, HostTiming::now() - t0), t0 = HostTiming::now();
     if (e != hipSuccess) return hip_status(e, op == Op::kSeal ? "seal" : "verify");
     const TableImage& tb = tables[sg.tag];
-    if (op == Op::kSeal) {
+    if (op == Op::kSeal && !post_on_host) {
+      // (written in place by the kernel)
+    } else if (op == Op::kSeal) {
       // [type][EncodeFixed32(masked crc)] (table_builder.cc:245-249)
       for (size_t b = 0; b < tb.n; b++) {
         uint32_t m;
@@ -210,10 +221,12 @@ bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op o
     if (op == Op::kSeal) memcpy(sg.zmeta.h + tb.n * sizeof(BlockHandle), tb.types, tb.n);
     const uint64_t* d_h = reinterpret_cast<const uint64_t*>(sg.zmeta.d);
     sg.settled = false;
-    const int rc = op == Op::kSeal
-                       ? lsbm_sst_trailer_crcs_dev(dev[t], tb.file_size, d_h, sg.zmeta.d + tb.n * sizeof(BlockHandle),
-                                                   tb.n, reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream)
-                       : lsbm_sst_verify_dev(dev[t], tb.file_size, d_h, tb.n, sg.res.d, nullptr, sg.stream);
+    const uint8_t* d_ty = sg.zmeta.d + tb.n * sizeof(BlockHandle);
+    const int rc = op == Op::kVerify ? lsbm_sst_verify_dev(dev[t], tb.file_size, d_h, tb.n, sg.res.d, nullptr, sg.stream)
+                   : post_on_host    ? lsbm_sst_trailer_crcs_dev(dev[t], tb.file_size, d_h, d_ty, tb.n,
+                                                                 reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream)
+                                     : sst_seal_in_place(const_cast<uint8_t*>(dev[t]), tb.file_size, d_h, d_ty, tb.n,
+                                                         sg.stream);
     if (rc != LSBM_OK) {
       *st = Status::IOError(lsbm_crc32c_last_error());
       return true;

@@ -244,6 +244,37 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(okh.data(), dok, okh.size(), hipMemcpyDeviceToHost);
         printf("{\"what\": \"zerocopy_check\", \"blocks_ok\": %zu, \"blocks\": %zu}\n",
                (size_t)std::count(okh.begin(), okh.end(), 1), okh.size());
+        // The DMA path's floor: the table's bytes alone over the copy engines,
+        // from this registered image and from a hipHostMalloc'd one, whole or
+        // in 4 chunks on one stream, and whole + the verify kernel behind it.
+        void* dbuf = nullptr;
+        void* hm = nullptr;
+        if (hipMalloc(&dbuf, t.img.size()) == hipSuccess &&
+            hipHostMalloc(&hm, t.img.size(), hipHostMallocDefault) == hipSuccess) {
+          memcpy(hm, t.img.data(), t.img.size());
+          auto dma = [&](const void* src, int pieces, bool kernel) {
+            const size_t n = t.img.size(), step = (n + pieces - 1) / pieces;
+            bool good = true;
+            for (size_t o = 0; o < n && good; o += step)
+              good = hipMemcpyAsync(static_cast<char*>(dbuf) + o, static_cast<const char*>(src) + o,
+                                    std::min(step, n - o), hipMemcpyHostToDevice, st) == hipSuccess;
+            if (good && kernel)
+              good = lsbm_sst_verify_dev(static_cast<const uint8_t*>(dbuf), n, dh, t.h.size(), dok, nullptr, st) ==
+                     LSBM_OK;
+            good = good && hipStreamSynchronize(st) == hipSuccess;
+            return good ? lsbm::Status::OK() : lsbm::Status::IOError("dma");
+          };
+          for (int w = 0; w < 3; w++) (void)dma(hm, 1, true);
+          if (!phase("dma_only_registered", [&] { return dma(t.img.data(), 1, false); })) return 1;
+          if (!phase("dma_only_registered_4", [&] { return dma(t.img.data(), 4, false); })) return 1;
+          if (!phase("dma_only_hostmalloc", [&] { return dma(hm, 1, false); })) return 1;
+          if (!phase("dma_verify_registered", [&] { return dma(t.img.data(), 1, true); })) return 1;
+          if (!phase("dma_verify_hostmalloc", [&] { return dma(hm, 1, true); })) return 1;
+        } else {
+          printf("{\"what\": \"dma_only\", \"status\": \"setup failed\"}\n");
+        }
+        (void)hipFree(dbuf);
+        if (hm) (void)hipHostFree(hm);
       } else {
         printf("{\"what\": \"zerocopy\", \"status\": \"setup failed\"}\n");
       }
