@@ -232,6 +232,10 @@ int lsbm_test_host_pinned(const void* p, size_t n);
  * place (zero copy) instead of DMA-ed in chunks (LSBM_ZERO_COPY_MAX_MB sets it
  * at start-up; 0 = never); returns -1 for mb < 0. */
 int lsbm_test_zero_copy_max_mb(int mb);
+/* Testing / measurement: the pageable layers' staging copy of n bytes (src ->
+ * dst, non-temporal stores), over the worker pool when `parallel` is nonzero,
+ * else on the calling thread.  Returns 0. */
+int lsbm_test_host_copy(void* dst, const void* src, size_t n, int parallel);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -659,6 +659,15 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_overlap(int
 }
 
 // Testing: host_pinned() itself (which ranges the layers DMA in place).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_host_copy(void* dst, const void* src, size_t n,
+                                                                      int parallel) {
+  if (parallel)
+    lsbm::parallel_copy(dst, src, n);
+  else
+    lsbm::stream_copy(static_cast<char*>(dst), static_cast<const char*>(src), n);
+  return 0;
+}
+
 extern "C" __attribute__((visibility("default"))) int lsbm_test_host_pinned(const void* p, size_t n) {
   return lsbm::host_pinned(p, n) ? 1 : 0;
 }

@@ -183,6 +183,28 @@ int main(int argc, char** argv) {
     print_phase(what, v, bytes, a, b, st.ToString().c_str(), check_table(t), starts);
     return st.ok();
   };
+  {
+    // The pageable layers' staging copy alone (the pageable seal's critical
+    // path): the table into a page-locked buffer over the pool, one chunk's
+    // worth over the pool, and on one thread.
+    void* stg = nullptr;
+    if (hipHostMalloc(&stg, t.img.size(), hipHostMallocDefault) == hipSuccess) {
+      auto copy_phase = [&](const char* what, size_t n, int par) {
+        std::vector<double> v;
+        for (int r = 0; r < reps; r++) {
+          const double t0 = now();
+          lsbm_test_host_copy(stg, t.img.data(), n, par);
+          v.push_back(now() - t0);
+        }
+        printf("{\"what\": \"%s\", \"bytes\": %zu, \"threads\": %d, \"dist\": %s}\n", what, n,
+               par ? lsbm_host_threads() + 1 : 1, dist_json(v, (double)n).c_str());
+      };
+      copy_phase("host_copy_table_pool", t.img.size(), 1);
+      copy_phase("host_copy_4MiB_pool", std::min<size_t>(t.img.size(), 4u << 20), 1);
+      copy_phase("host_copy_table_one_thread", t.img.size(), 0);
+      (void)hipHostFree(stg);
+    }
+  }
   for (int locked = 0; locked < 2; locked++) {
     if (locked && hipHostRegister(t.img.data(), t.img.size(), hipHostRegisterDefault) != hipSuccess) {
       fprintf(stderr, "hipHostRegister failed\n");

@@ -17,7 +17,7 @@ for p in 1 2; do
 done
 for f in $OUT/*_p*.log; do echo "$(basename $f) $(grep -o '"ms": [0-9.]*\|"frac": [0-9.]*' $f | paste -sd' ')"; done
 timeout -k 10 180 build/bench_one_table 100 4 > $OUT/one_table.log 2>&1
-rc=$?; echo "one_table rc=$rc"; cut -c1-230 $OUT/one_table.log | grep -E "locked|dma"; [ $rc -eq 0 ] || exit $rc
+rc=$?; echo "one_table rc=$rc"; cut -c1-230 $OUT/one_table.log | grep -E "locked|dma|host_copy"; [ $rc -eq 0 ] || exit $rc
 LSBM_ZERO_COPY_SEAL_POST=1 timeout -k 10 180 build/bench_one_table 100 4 > $OUT/one_table_post.log 2>&1
 rc=$?; echo "one_table post rc=$rc"; cut -c1-230 $OUT/one_table_post.log | grep -E "_locked"; [ $rc -eq 0 ] || exit $rc
 LSBM_ZERO_COPY_MAX_MB=0 timeout -k 10 180 build/bench_one_table 100 4 > $OUT/one_table_dma.log 2>&1
