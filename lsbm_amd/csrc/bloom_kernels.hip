@@ -469,6 +469,19 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 #ifndef LSBM_BUILD_DEPTH  // (A/B builds override)
 #define LSBM_BUILD_DEPTH 1
 #endif
+#ifndef LSBM_BUILD_LDS_FOLD  // (A/B builds override)
+#define LSBM_BUILD_LDS_FOLD 1
+#endif
+// LDS byte address of p (a pointer into __shared__ memory), and the LDS word
+// holding bit b (an LDS bit address) or-ed with v
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
+  return (uint32_t)(uintptr_t)(const lds_u32*)p;
+}
+__device__ __forceinline__ void lds_or(uint32_t b, uint32_t v) {
+  lds_u32* w = (lds_u32*)(uintptr_t)((b >> 3) & ~3u);
+  (void)__hip_atomic_fetch_or(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 #ifndef LSBM_BUILD_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_BUILD_WAVES_PER_EU 7
 #endif
@@ -569,7 +582,13 @@ void bloom_build_kernel(BloomBuildArgs a) {
       const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
       const uint64_t m_t = fastmod_magic(d_t);
       const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
+#if LSBM_BUILD_LDS_FOLD
+      // (the bit base counts from LDS address 0: a probe's word address is
+      // then (b >> 3) & ~3 with no region base added, one VALU per probe less)
+      slots[wv][lane] = make_uint4(8u * (lds_addr(bm) + byte_t), d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
+#else
       slots[wv][lane] = make_uint4(8u * byte_t, d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
+#endif
       slot_c32[wv][lane] = c == d_t ? 0u : c;
     }
     const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
@@ -671,7 +690,11 @@ void bloom_build_kernel(BloomBuildArgs a) {
 #else
       for (uint32_t q = 0; q < a.k; q++) {
         const uint32_t b = bbase + ps.pos;
+#if LSBM_BUILD_LDS_FOLD
+        lds_or(b, 1u << (b & 31u));
+#else
         atomicOr(&bm[b >> 5], 1u << (b & 31u));
+#endif
         ps.next();
       }
 #endif

@@ -15,6 +15,12 @@ for p in 1 2; do
     LSBM_LIB_PATH=$L timeout -k 10 300 python -u tools/bench_bloom.py probe block --cpu-filters 0 > $OUT/${v}_p$p.log 2>&1 || exit 1
   done
 done
+for p in 1 2; do
+  for v in default nofold; do
+    if [ $v = default ]; then L=""; else L="$PWD/build/abl/$v/liblsbm_crc32c.so"; fi
+    LSBM_LIB_PATH=$L timeout -k 10 300 python -u tools/bench_bloom.py build --cpu-filters 0 > $OUT/build_${v}_p$p.log 2>&1 || exit 1
+  done
+done
 for f in $OUT/*_p*.log; do echo "$(basename $f) $(grep -o '"ms": [0-9.]*\|"frac": [0-9.]*' $f | paste -sd' ')"; done
 timeout -k 10 180 build/bench_one_table 100 4 > $OUT/one_table.log 2>&1
 rc=$?; echo "one_table rc=$rc"; cut -c1-230 $OUT/one_table.log | grep -E "locked|dma|host_copy"; [ $rc -eq 0 ] || exit $rc
