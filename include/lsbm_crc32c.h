@@ -228,9 +228,11 @@ int lsbm_test_pool_overlap(int callers, int jobs, int pieces, int piece_us, doub
 /* Testing: 1 if the C++ layers would DMA [p, p + n) in place (page-locked by
  * hipHostMalloc or one hipHostRegister covering the whole range), else 0. */
 int lsbm_test_host_pinned(const void* p, size_t n);
-/* Testing: page-locked table jobs up to `mb` MiB are read by the kernel in
- * place (zero copy) instead of DMA-ed in chunks (LSBM_ZERO_COPY_MAX_MB sets it
- * at start-up; 0 = never); returns -1 for mb < 0. */
+/* Testing: page-locked table jobs up to `mb` MiB take the small-job path
+ * (each table one whole-image DMA and one kernel on a stage's stream, or with
+ * LSBM_SMALL_LOCKED=zc read by the kernel in place) instead of the chunk
+ * pipeline (LSBM_ZERO_COPY_MAX_MB sets it at start-up; 0 = never); returns -1
+ * for mb < 0. */
 int lsbm_test_zero_copy_max_mb(int mb);
 /* Testing / measurement: the pageable layers' staging copy of n bytes (src ->
  * dst, non-temporal stores), over the worker pool when `parallel` is nonzero,

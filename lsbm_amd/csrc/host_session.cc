@@ -82,39 +82,48 @@ thread_local int t_job_node = -1;
 
 struct Job {
   const std::function<void(size_t)>* fn;
-  size_t pieces, next, finished;
+  size_t pieces;
   int node;
+  std::atomic<size_t> next{0}, finished{0};
+  std::atomic<int> users{0};   // workers holding this job (picked under mu_)
+  std::atomic<int> active{0};  // pieces in progress (testing: pool_take_peak_jobs)
 };
 
+// Pieces are claimed and counted with atomics; mu_ guards only the job list
+// (one push and one removal per job, one pick per worker and job).  Round 4:
+// a mutex round trip per piece -- 16 threads on one std::mutex, each loser
+// parked in the kernel -- cost ~50 us per parallel_for, so a 4 MiB staging
+// copy took 64 us on 16 threads against 54 us on one
+// (profiles/r04/check11/one_table.log, host_copy_*).
 class WorkPool {
  public:
   void run(size_t pieces, const std::function<void(size_t)>& fn, int node) {
-    Job j{&fn, pieces, 0, 0, node};
+    Job j;
+    j.fn = &fn;
+    j.pieces = pieces;
+    j.node = node;
     {
       std::lock_guard<std::mutex> l(mu_);
       start_locked();
       jobs_.push_back(&j);
-      live_.push_back(&j);
       queued_.store(jobs_.size(), std::memory_order_release);
     }
     if (pieces > 2) work_cv_.notify_all();
     else work_cv_.notify_one();
     t_in_pool = true;
-    for (;;) {  // the caller's share: pieces of its own job only
-      size_t k;
-      {
-        std::lock_guard<std::mutex> l(mu_);
-        if (j.next >= j.pieces) break;
-        k = take_locked(&j);
-      }
-      fn(k);
-      std::lock_guard<std::mutex> l(mu_);
-      if (++j.finished == j.pieces) done_cv_.notify_all();
-    }
+    work_on(&j);  // the caller's share: pieces of its own job only
     t_in_pool = false;
-    std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [&] { return j.finished == j.pieces; });
-    live_.erase(std::find(live_.begin(), live_.end(), &j));
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      drop_locked(&j);  // (no worker picks it up from here on)
+    }
+    // the pieces still running elsewhere, and the workers still holding j
+    for (uint32_t i = 1; j.finished.load(std::memory_order_acquire) != pieces ||
+                         j.users.load(std::memory_order_acquire) != 0;
+         i++) {
+      _mm_pause();
+      if ((i & 1023u) == 0) std::this_thread::yield();
+    }
   }
   int threads() {
     std::lock_guard<std::mutex> l(mu_);
@@ -122,25 +131,28 @@ class WorkPool {
     return (int)workers_;
   }
   // Testing: the most jobs that had pieces running at once since the last call.
-  int take_peak() {
-    std::lock_guard<std::mutex> l(mu_);
-    const int p = active_max_;
-    active_max_ = 0;
-    return p;
-  }
+  int take_peak() { return active_max_.exchange(0); }
 
  private:
-  // next piece of j (mu_ held); drops j from the queue when it is handed out
-  size_t take_locked(Job* j) {
-    const size_t k = j->next++;
-    if (j->next == j->pieces) {
-      jobs_.erase(std::find(jobs_.begin(), jobs_.end(), j));
-      queued_.store(jobs_.size(), std::memory_order_release);
+  void work_on(Job* j) {
+    for (;;) {
+      const size_t k = j->next.fetch_add(1, std::memory_order_relaxed);
+      if (k >= j->pieces) return;
+      if (j->active.fetch_add(1) == 0) {
+        const int r = running_.fetch_add(1) + 1;
+        int m = active_max_.load();
+        while (r > m && !active_max_.compare_exchange_weak(m, r)) {
+        }
+      }
+      (*j->fn)(k);
+      if (j->active.fetch_sub(1) == 1) running_.fetch_sub(1);
+      j->finished.fetch_add(1, std::memory_order_release);
     }
-    int running = 0;  // jobs with a piece in progress (testing: pool_take_peak_jobs)
-    for (Job* q : live_) running += q->next > q->finished;
-    active_max_ = std::max(active_max_, running);
-    return k;
+  }
+  void drop_locked(Job* j) {
+    auto it = std::find(jobs_.begin(), jobs_.end(), j);
+    if (it != jobs_.end()) jobs_.erase(it);
+    queued_.store(jobs_.size(), std::memory_order_release);
   }
   Job* pick_locked(int node) {
     for (Job* q : jobs_)
@@ -187,8 +199,6 @@ class WorkPool {
     t_in_pool = true;
     NumaBind nb(bind ? node : -1, true, false);  // (kept bound for the thread's life)
     for (;;) {
-      Job* j;
-      size_t k;
       if (queued_.load(std::memory_order_acquire) == 0 && spin_us() > 0) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t i = 1; queued_.load(std::memory_order_acquire) == 0; i++) {
@@ -198,25 +208,28 @@ class WorkPool {
             break;
         }
       }
+      Job* j;
       {
         std::unique_lock<std::mutex> l(mu_);
         work_cv_.wait(l, [&] { return !jobs_.empty(); });
         j = pick_locked(node);
-        k = take_locked(j);
+        j->users.fetch_add(1, std::memory_order_relaxed);
       }
-      (*j->fn)(k);
-      std::lock_guard<std::mutex> l(mu_);
-      if (++j->finished == j->pieces) done_cv_.notify_all();
+      work_on(j);
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        drop_locked(j);  // (exhausted: others look elsewhere)
+      }
+      j->users.fetch_sub(1, std::memory_order_release);  // (j may be gone after this)
     }
   }
   std::mutex mu_;
-  std::condition_variable work_cv_, done_cv_;
-  std::vector<Job*> jobs_;  // jobs with pieces not yet handed out, oldest first
-  std::vector<Job*> live_;  // jobs not yet collected by their caller
+  std::condition_variable work_cv_;
+  std::vector<Job*> jobs_;  // jobs whose pieces may not all be claimed yet, oldest first
   std::atomic<size_t> queued_{0};  // jobs_.size(), for the workers' spin
   size_t workers_ = 0;
   bool started_ = false;
-  int active_max_ = 0;
+  std::atomic<int> running_{0}, active_max_{0};
 };
 
 WorkPool* pool() {

@@ -128,7 +128,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
 enum class Op { kSeal, kVerify };
 
 // Page-locked jobs up to this many bytes (LSBM_ZERO_COPY_MAX_MB, default 64;
-// 0 = never) are read by the kernel in place, see run_zero_copy.
+// 0 = never) take run_small_locked instead of the chunk pipeline.
 std::atomic<long> g_zero_copy_mb{-1};  // -1: not read yet
 size_t zero_copy_max() {
   long v = g_zero_copy_mb.load(std::memory_order_relaxed);
@@ -142,20 +142,32 @@ size_t zero_copy_max() {
 }
 
 // A small page-locked job -- one table per call, as TableBuilder::Finish
-// makes them (lsbm/db_impl.cc:843-892) -- needs no DMA and no device copy:
-// the kernel reads each image in place over PCIe through its device mapping,
-// its handles and types from a mapped page-locked buffer, and writes the
-// results into another (one launch per table, spread over the stages, then
-// one wait each).  A 16 MiB table: 0.38-0.39 ms, flat call to call, against
-// 0.45-0.62 ms through DMA chunks from the same registered image, whose
-// per-chunk DMA -> kernel order serialises the call (profiles/r04/check6,
-// the zerocopy_* lines).  A kernel's own PCIe reads peak lower than the DMA
-// engines (~46 against ~57 GB/s), so big jobs keep the DMA pipeline.
-// Returns false, having done nothing, when an image has no device mapping.
-bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op op, std::vector<uint8_t>* ok_out,
-                   const std::vector<size_t>& ok_base, size_t* nbad_out, HostTiming& tm, Status* st) {
+// makes them (lsbm/db_impl.cc:843-892): each table is ONE DMA of its whole
+// image on a stage's stream and one kernel behind it, its handles and types
+// read by the kernel from a mapped page-locked buffer and its results
+// written into another (no metadata DMA, no cross-stream events), tables
+// spread over the stages, then one wait each.  A 16 MiB table's DMA alone
+// takes 0.301 ms (55.7 GB/s), the DMA and the verify kernel 0.334 ms, where
+// 4 back-to-back DMAs of its quarters take 0.334 ms alone and the kernel's
+// own PCIe reads of the image in place (zero copy) 0.39-0.43 ms
+// (profiles/r04/check11/one_table.log: dma_* and zerocopy_* lines).
+// LSBM_SMALL_LOCKED=zc (A/B): the kernel reads the image in place through its
+// device mapping, the seal storing its trailers there as plain byte stores.
+// Returns false, having done nothing, when zero copy is asked for and an
+// image has no device mapping.
+bool small_locked_zero_copy() {
+  static const bool zc = [] {
+    const char* e = getenv("LSBM_SMALL_LOCKED");
+    return e && strcmp(e, "zc") == 0;
+  }();
+  return zc;
+}
+
+bool run_small_locked(HostSession& hs, const TableImage* tables, size_t count, Op op, std::vector<uint8_t>* ok_out,
+                      const std::vector<size_t>& ok_base, size_t* nbad_out, HostTiming& tm, Status* st) {
+  const bool zc = small_locked_zero_copy();
   std::vector<const uint8_t*> dev(count, nullptr);
-  for (size_t t = 0; t < count; t++) {
+  for (size_t t = 0; t < count && zc; t++) {
     if (tables[t].n == 0) continue;
     // (only memory page-locked for this very device: another device's
     // mapping is not this one's)
@@ -169,22 +181,14 @@ bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op o
     dev[t] = static_cast<const uint8_t*>(p);
   }
   size_t nbad = 0;
-  // The seal writes its trailers into the image itself, over PCIe (each wave
-  // its own blocks' 5 bytes, posted writes): no host pass over the table's
-  // trailer pages after the kernel.  LSBM_ZERO_COPY_SEAL_POST=1 (A/B): dense
-  // CRCs into a mapped buffer, posted by this thread.
-  static const bool post_on_host = [] {
-    const char* e = getenv("LSBM_ZERO_COPY_SEAL_POST");
-    return e && atoi(e) != 0;
-  }();
   auto collect = [&](Stage& sg) -> Status {
     double t0 = tm.on ? HostTiming::now() : 0.0;
     const hipError_t e = hs.wait(sg);
     if (tm.on) tm.add(HostTiming::kWait, HostTiming::now() - t0), t0 = HostTiming::now();
     if (e != hipSuccess) return hip_status(e, op == Op::kSeal ? "seal" : "verify");
     const TableImage& tb = tables[sg.tag];
-    if (op == Op::kSeal && !post_on_host) {
-      // (written in place by the kernel)
+    if (op == Op::kSeal && zc) {
+      // (stored in place by the kernel)
     } else if (op == Op::kSeal) {
       // [type][EncodeFixed32(masked crc)] (table_builder.cc:245-249)
       for (size_t b = 0; b < tb.n; b++) {
@@ -213,6 +217,7 @@ bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op o
     if (sg.busy && !(*st = collect(sg)).ok()) return true;
     hipError_t e = sg.zmeta.reserve_mapped(tb.n * (sizeof(BlockHandle) + 1) + 16);
     if (e == hipSuccess) e = sg.res.reserve_mapped(tb.n * 4 + 16);
+    if (e == hipSuccess && !zc) e = sg.bulk.reserve(tb.file_size + 64);  // (+ the kernel's row slack)
     if (e != hipSuccess) {
       *st = hip_status(e, "staging buffers");
       return true;
@@ -220,13 +225,21 @@ bool run_zero_copy(HostSession& hs, const TableImage* tables, size_t count, Op o
     memcpy(sg.zmeta.h, tb.handles, tb.n * sizeof(BlockHandle));
     if (op == Op::kSeal) memcpy(sg.zmeta.h + tb.n * sizeof(BlockHandle), tb.types, tb.n);
     const uint64_t* d_h = reinterpret_cast<const uint64_t*>(sg.zmeta.d);
-    sg.settled = false;
     const uint8_t* d_ty = sg.zmeta.d + tb.n * sizeof(BlockHandle);
-    const int rc = op == Op::kVerify ? lsbm_sst_verify_dev(dev[t], tb.file_size, d_h, tb.n, sg.res.d, nullptr, sg.stream)
-                   : post_on_host    ? lsbm_sst_trailer_crcs_dev(dev[t], tb.file_size, d_h, d_ty, tb.n,
-                                                                 reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream)
-                                     : sst_seal_in_place(const_cast<uint8_t*>(dev[t]), tb.file_size, d_h, d_ty, tb.n,
-                                                         sg.stream);
+    sg.settled = false;
+    const uint8_t* img = dev[t];
+    if (!zc) {
+      e = hipMemcpyAsync(sg.bulk.d, tb.file, tb.file_size, hipMemcpyHostToDevice, sg.stream);
+      if (e != hipSuccess) {
+        *st = hip_status(e, "H2D");
+        return true;
+      }
+      img = sg.bulk.d;
+    }
+    const int rc = op == Op::kVerify ? lsbm_sst_verify_dev(img, tb.file_size, d_h, tb.n, sg.res.d, nullptr, sg.stream)
+                   : zc ? sst_seal_in_place(const_cast<uint8_t*>(img), tb.file_size, d_h, d_ty, tb.n, sg.stream)
+                        : lsbm_sst_trailer_crcs_dev(img, tb.file_size, d_h, d_ty, tb.n,
+                                                    reinterpret_cast<uint32_t*>(sg.res.d), nullptr, sg.stream);
     if (rc != LSBM_OK) {
       *st = Status::IOError(lsbm_crc32c_last_error());
       return true;
@@ -272,8 +285,8 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
       all_pinned = all_pinned && (tables[t].n == 0 || pinned[t]);
     }
     if (all_pinned && total <= zero_copy_max() &&
-        run_zero_copy(*s, tables, count, op, ok_out, ok_base, nbad_out, tm, &st))
-      return st;  // (false: an image without a device mapping; the DMA pipeline below)
+        run_small_locked(*s, tables, count, op, ok_out, ok_base, nbad_out, tm, &st))
+      return st;  // (false: zero copy asked for and an image without a device mapping)
   }
   const size_t meta_bytes = plan.max_blocks * (sizeof(BlockHandle) + 1) + 16;
   const size_t res_bytes = plan.max_blocks * 4 + 16;

@@ -423,9 +423,9 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
     assert r.stdout.startswith("OK")
 
 
-@pytest.mark.parametrize("pinned,zero_copy_mb", [(0, 64), (1, 64), (1, 0)],
-                         ids=["pageable", "locked-zero-copy", "locked-dma"])
-def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb):
+@pytest.mark.parametrize("pinned,zero_copy_mb,small", [(0, 64, ""), (1, 64, ""), (1, 64, "zc"), (1, 0, "")],
+                         ids=["pageable", "locked-small-dma", "locked-small-zero-copy", "locked-chunks"])
+def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb, small):
     """4 threads each sealing their own 16 MiB table, one table per call
     (tests/cpp/concurrent_seal_test.cc): trailers byte-identical to the same
     calls made one after another and to util/crc32c.h's WriteRawBlock pattern,
@@ -433,9 +433,10 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb
     per table, and the concurrent calls take measurably less wall time (each
     caller leases its own session of the device) -- pageable images, where one
     caller's host copy leaves PCIe idle part of the time.  Page-locked images
-    are DMA-ed in place: one caller alone already runs near the PCIe ceiling
-    (~45 of ~52 GB/s, profiles/r04/), so there concurrency must only not
-    cost anything."""
+    are DMA-ed in place (each table whole, or, small=zc, read by the kernel
+    in place; or, zero_copy_mb=0, in chunks through the pipeline): one caller
+    alone already runs near the PCIe ceiling (profiles/r04/), so there
+    concurrency must only not cost anything."""
     import os
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -446,8 +447,11 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb
                     os.path.join(repo, "tests", "cpp", "concurrent_seal_test.cc"), "-L", libdir,
                     "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
                     "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    env = dict(os.environ)
+    if small:
+        env["LSBM_SMALL_LOCKED"] = small
     r = subprocess.run([str(exe), "4", "8", str(pinned), str(zero_copy_mb)], capture_output=True, text=True,
-                       timeout=120)
+                       timeout=120, env=env)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK"), r.stdout
