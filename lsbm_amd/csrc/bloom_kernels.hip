@@ -469,9 +469,6 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 #ifndef LSBM_BUILD_DEPTH  // (A/B builds override)
 #define LSBM_BUILD_DEPTH 1
 #endif
-#ifndef LSBM_BUILD_LDS_FOLD  // (A/B builds override)
-#define LSBM_BUILD_LDS_FOLD 1
-#endif
 // LDS byte address of p (a pointer into __shared__ memory), and the LDS word
 // holding bit b (an LDS bit address) or-ed with v
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -491,7 +488,7 @@ __global__ __launch_bounds__(kBloomThreads) __attribute__((amdgpu_waves_per_eu(L
 void bloom_build_kernel(BloomBuildArgs a) {
   // (rows of kBloomRegionWords: 16-B aligned, for the staging area's b128 writes)
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBloomWaves][kBloomRegionWords];
-  // the group's filter constants, one slot per filter: LDS word base, bits d,
+  // the group's filter constants, one slot per filter: its first bit as an LDS bit address, bits d,
   // fastmod magic (lo, hi); and 2^32 mod d.  (Read by index rather than with
   // bpermute from the filter's lane: 5 fewer VGPRs live across the rounds,
   // 0.354 -> 0.348 ms, profiles/r02/bloom/ab_slots.log.)
@@ -582,13 +579,10 @@ void bloom_build_kernel(BloomBuildArgs a) {
       const uint32_t d_t = lane < g ? (uint32_t)(bytes * 8) : 64u;
       const uint64_t m_t = fastmod_magic(d_t);
       const uint32_t c = fastmod(0xffffffffu, m_t, d_t) + 1;
-#if LSBM_BUILD_LDS_FOLD
       // (the bit base counts from LDS address 0: a probe's word address is
-      // then (b >> 3) & ~3 with no region base added, one VALU per probe less)
+      // then (b >> 3) & ~3 with no region base added, one VALU per probe
+      // less: 0.300 -> 0.295-0.298 ms, profiles/r04/check11/build_*.log)
       slots[wv][lane] = make_uint4(8u * (lds_addr(bm) + byte_t), d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
-#else
-      slots[wv][lane] = make_uint4(8u * byte_t, d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
-#endif
       slot_c32[wv][lane] = c == d_t ? 0u : c;
     }
     const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
@@ -690,11 +684,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
 #else
       for (uint32_t q = 0; q < a.k; q++) {
         const uint32_t b = bbase + ps.pos;
-#if LSBM_BUILD_LDS_FOLD
         lds_or(b, 1u << (b & 31u));
-#else
-        atomicOr(&bm[b >> 5], 1u << (b & 31u));
-#endif
         ps.next();
       }
 #endif
@@ -796,94 +786,6 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
   return true;
 }
 
-// key_may_match for the common filter: fewer than 2^31 bits, and every bit
-// addressable as a 32-bit bit index fb + pos from a 4-byte aligned base b4
-// (fb = 8 * (f - b4)).  Each probe loads the aligned dword holding its bit
-// (a dword never crosses a page, so it reads no page the filter does not
-// touch) and tests bit B & 31 of it: per probe the bit index, its dword's
-// byte offset, the mask and the 5-op ProbeSeq step, ~9 VALU against ~14 with
-// a 64-bit byte address and the carry-corrected step.  Same answers as
-// key_may_match (util/bloom.cc:65-89).
-#ifndef LSBM_PROBE_FAST  // (A/B builds override)
-#define LSBM_PROBE_FAST 1
-#endif
-#ifndef LSBM_PROBE_FAST_INLINE  // (A/B builds override)
-#define LSBM_PROBE_FAST_INLINE 0
-#endif
-#if LSBM_PROBE_FAST_INLINE
-__device__ __forceinline__
-#else
-__device__ __attribute__((noinline))
-#endif
-bool key_may_match32(uint64_t b4, uint32_t fb, uint32_t len, uint32_t h, uint64_t k_use) {
-  // (b4 and k_use are the same in every lane: scalar, so that the loads take
-  // b4 as their scalar base and the probe count is a scalar branch)
-  b4 = readlane64(b4, __builtin_amdgcn_readfirstlane(threadIdx.x) & 63u);
-  k_use = readlane64(k_use, __builtin_amdgcn_readfirstlane(threadIdx.x) & 63u);
-  if (len < 2) return false;
-  const uint32_t bits = (len - 1) * 8;
-  BitMod m;
-  m.big = false;
-  m.d = bits;
-  {  // 1 / bits from the hardware reciprocal and one Newton step (relative
-     // error ~2^-44; mod_bits needs < 2^-29 for its one correction step)
-    const double dd = (double)bits;
-    const double r0 = __builtin_amdgcn_rcp(dd);
-    m.rcp = __builtin_fma(r0, __builtin_fma(-dd, r0, 1.0), r0);
-  }
-  const uint32_t delta = (h >> 17) | (h << 15);
-  const uint32_t c = mod_bits(0xffffffffu, m) + 1;  // 2^32 mod bits
-  ProbeSeq ps = probe_seq(h, delta, mod_bits(h, m), mod_bits(delta, m), c == bits ? 0 : c, bits);
-  const uint32_t k0n = k_use < 16 ? (uint32_t)k_use : 16u;
-  const uint8_t kb = *reinterpret_cast<gcu8>(b4 + (fb >> 3) + len - 1);
-  uint32_t v[16], bit[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    bit[j] = 0u;
-    v[j] = 0u;
-    if ((uint32_t)j < k0n) {  // (k_use is the same in every lane)
-      const uint32_t B = fb + ps.pos;
-      bit[j] = 1u << (B & 31u);
-      v[j] = *reinterpret_cast<gcu32>(b4 + ((B >> 3) & ~3u));
-      ps.next();
-    }
-  }
-  const uint64_t stored = (uint64_t)(int64_t)(int8_t)kb;
-  const uint64_t k = stored > k_use ? k_use : stored;
-  if (k > 30) return true;
-  bool all = true;
-#pragma unroll
-  for (int j = 0; j < 16; j++) all &= (uint32_t)j >= k || (v[j] & bit[j]) != 0u;
-  if (!all) return false;
-  for (uint32_t j0 = k0n; j0 < (uint32_t)k; j0 += 16) {  // (k_use > 16 only)
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      bit[j] = 0u;
-      v[j] = 0u;
-      if (j0 + j < (uint32_t)k) {
-        const uint32_t B = fb + ps.pos;
-        bit[j] = 1u << (B & 31u);
-        v[j] = *reinterpret_cast<gcu32>(b4 + ((B >> 3) & ~3u));
-        ps.next();
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j++) all &= j0 + j >= (uint32_t)k || (v[j] & bit[j]) != 0u;
-    if (!all) return false;
-  }
-  return true;
-}
-
-// The filter [f, f + len) by key_may_match32 when it qualifies, else the
-// general form.
-__device__ __forceinline__ bool filter_may_match(uint64_t b4, uint64_t f, uint64_t len, uint32_t h, uint64_t k_use) {
-#if LSBM_PROBE_FAST
-  if (f >= b4 && len < (1ull << 28) && f - b4 + len < (1ull << 29))
-    return key_may_match32(b4, (uint32_t)(f - b4) * 8u, (uint32_t)len, h, k_use);
-#endif
-  return key_may_match(f, len, h, k_use);
-}
-
 constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 31-B keys + slack)
 
 // One instantiation per mode (the other mode's code dropped).  The
@@ -894,9 +796,6 @@ constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 3
 // its registers (profiles/r02/bloom/ab_probe_pipelined.log).
 #ifndef LSBM_PROBE_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_WAVES_PER_EU 6
-#endif
-#ifndef LSBM_PROBE_HANDLE_AHEAD  // (A/B builds override)
-#define LSBM_PROBE_HANDLE_AHEAD 0
 #endif
 #ifndef LSBM_PROBE_BLOCK_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_BLOCK_WAVES_PER_EU 1
@@ -911,9 +810,6 @@ void bloom_probe_kernel(BloomProbeArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t hits = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  // (key_may_match32's base: scalar, from the kernel arguments)
-  const uint64_t b4 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(a.base) >> 32)) << 32 |
-                      (__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(a.base)) & ~3u);
   // wave-uniform rounds of 64 consecutive queries (the hash is a wave operation)
 #ifndef LSBM_PROBE_NO_PIPELINE  // A/B builds only
   // Pipelined like the build: a round's key offsets are loaded two rounds
@@ -934,40 +830,17 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     plan = plan_span(kbase + oa0, n, avail, safe);
     fetch_span(plan, ch0, ch1);
   }
-#if LSBM_PROBE_HANDLE_AHEAD
-  // the filter handle (and data offset) one round ahead too: a round's probe
-  // loads then wait only for its hash, not for a handle load behind it
-  uint64_t hc, hs, hd = 0;
-  {
-    const uint64_t qq = q00 + lane < a.n ? q00 + lane : 0;
-    hc = a.handles[2 * qq];
-    hs = a.handles[2 * qq + 1];
-    if (a.mode != kProbeFilter) hd = a.data_offsets[qq];
-  }
-#endif
   for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
     const uint64_t ks = kbase + oa0;
     const uint64_t kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
-#if LSBM_PROBE_HANDLE_AHEAD
-    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + hc;
-    const uint64_t size = hs;
-    const uint64_t doff = hd;
-    {
-      const uint64_t qn = q + stride < a.n ? q + stride : 0;
-      hc = a.handles[2 * qn];
-      hs = a.handles[2 * qn + 1];
-      if (a.mode != kProbeFilter) hd = a.data_offsets[qn];
-    }
-#else
     // the filter handle (and data offset) do not depend on the hash: requested
     // before it (the hash's LDS fences would otherwise hold them back)
     const uint64_t qq = act ? q : 0;
     const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
     const uint64_t size = a.handles[2 * qq + 1];
     const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
-#endif
     // this round's chunks go to LDS; the next round's plan and loads go out
     const SpanPlan cur = plan;
     const u32x4 cc0 = ch0, cc1 = ch1;
@@ -997,7 +870,7 @@ void bloom_probe_kernel(BloomProbeArgs a) {
 #endif
     bool may;
     if (a.mode == kProbeFilter) {
-      may = filter_may_match(b4, c, size, h, a.k_use);
+      may = key_may_match(c, size, h, a.k_use);
     } else {
       // FilterBlockReader (table/filter_block.cc:78-109): "errors are treated
       // as potential matches"; base_lg is a size_t loaded from a char, and the
@@ -1013,7 +886,7 @@ void bloom_probe_kernel(BloomProbeArgs a) {
             const uint64_t start = load_le32(c + last_word + index * 4);
             const uint64_t limit = load_le32(c + last_word + index * 4 + 4);
             if (start <= limit && limit <= last_word)
-              may = filter_may_match(b4, c + start, limit - start, h, a.k_use);
+              may = key_may_match(c + start, limit - start, h, a.k_use);
             else if (start == limit)
               may = false;  // an empty filter matches nothing
           }

@@ -130,22 +130,27 @@ class WorkPool {
     start_locked();
     return (int)workers_;
   }
-  // Testing: the most jobs that had pieces running at once since the last call.
-  int take_peak() { return active_max_.exchange(0); }
+  // Testing: the most jobs that had pieces running at once since the last
+  // call (counted from the first call on).
+  int take_peak() {
+    track_.store(true);
+    return active_max_.exchange(0);
+  }
 
  private:
   void work_on(Job* j) {
     for (;;) {
       const size_t k = j->next.fetch_add(1, std::memory_order_relaxed);
       if (k >= j->pieces) return;
-      if (j->active.fetch_add(1) == 0) {
+      const bool track = track_.load(std::memory_order_relaxed);  // (tests only: shared counters)
+      if (track && j->active.fetch_add(1) == 0) {
         const int r = running_.fetch_add(1) + 1;
         int m = active_max_.load();
         while (r > m && !active_max_.compare_exchange_weak(m, r)) {
         }
       }
       (*j->fn)(k);
-      if (j->active.fetch_sub(1) == 1) running_.fetch_sub(1);
+      if (track && j->active.fetch_sub(1) == 1) running_.fetch_sub(1);
       j->finished.fetch_add(1, std::memory_order_release);
     }
   }
@@ -230,6 +235,7 @@ class WorkPool {
   size_t workers_ = 0;
   bool started_ = false;
   std::atomic<int> running_{0}, active_max_{0};
+  std::atomic<bool> track_{false};
 };
 
 WorkPool* pool() {
