@@ -228,22 +228,6 @@ __device__ __forceinline__ uint32_t mod_bits(uint32_t h, const BitMod& m) {
 // M = ceil(2^64 / d) computed once per filter (Lemire, Kaser & Kurz, "Faster
 // remainder by direct computation", 2019: exact for every 32-bit n and d).
 __device__ __forceinline__ uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
-
-// n % d in single precision, for 640 < d < 2^24 and rcp = 1/d correctly
-// rounded: float(n) is within 128 of n, and rcp and the product each within
-// 2^-24 relative, so float(n) * rcp is within (128 + 2^32 * 2^-23) / d < 1 of
-// n / d; its truncation q is the quotient or one off, and n - q * d (24-bit
-// multiply: q < 2^23, d < 2^24; mod 2^32) is fixed up by one step each way.
-// 9 full-rate VALU against fastmod's chain of 64-bit multiplies (quarter
-// rate on CDNA).  tests/test_bloom.py checks the arithmetic exhaustively over
-// sampled d.
-__device__ __forceinline__ uint32_t fmod_f32(uint32_t n, float rcp, uint32_t d) {
-  const uint32_t q = (uint32_t)((float)n * rcp);
-  uint32_t r = n - __umul24(q, d);
-  r = min(r, r + d);  // (q one too large: r wrapped below 0)
-  r = min(r, r - d);  // (q one too small: r >= d)
-  return r;
-}
 __device__ __forceinline__ uint32_t fastmod(uint32_t n, uint64_t M, uint32_t d) {
   const uint64_t low = M * n;  // mod 2^64
   const uint64_t lo = (uint64_t)(uint32_t)low * d, hi = (low >> 32) * d;
@@ -388,33 +372,20 @@ __device__ __forceinline__ void load_off2(const uint64_t* ko, uint64_t i, uint64
 struct SpanPlan {
   uint64_t sbase;  // 16-B aligned start (staged), or a safe 16-B aligned address
   uint32_t nch;    // chunks, 0 when not staged
-  uint32_t n0;     // staged and every active lane's key n0 bytes long: n0 (> 0), else 0
 };
 
-// (ballots of single compares, combined as scalar masks: a ballot of a
-// compound condition costs a select and a compare more per ballot)
-// kUniform: also decide the uniform-length hash here, a round ahead (the
-// build; the probe decides it in staged_hash, one register fewer across its
-// rounds: it has none to spare at 6 waves per SIMD)
-template <bool kUniform>
-__device__ __forceinline__ SpanPlan plan_span(uint64_t s, uint64_t n, uint32_t cap, uint64_t safe, bool act) {
-  const uint64_t nz = __ballot(n != 0);
+__device__ __forceinline__ SpanPlan plan_span(uint64_t s, uint64_t n, uint32_t cap, uint64_t safe) {
+  const uint64_t nz = __ballot(n > 0);
   const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
   const uint32_t ll = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
   const uint64_t lo = readlane64(s, fl), hi = readlane64(s + n, ll);
   const uint64_t sbase = lo & ~15ull;
-  // a non-empty key outside [lo, hi) (the lanes' keys out of order)
-  const uint64_t outside = (__ballot(s < lo) | __ballot(s + n > hi)) & nz;
-  const bool staged = nz != 0 && hi > lo && hi - sbase <= cap && hi - sbase <= 2048u && outside == 0ull;
+  const bool inside = n == 0 || (s >= lo && s + n <= hi);
+  const bool staged = nz != 0 && hi > lo && hi - sbase <= cap && hi - sbase <= 2048u &&
+                      __ballot(!inside) == 0ull;
   SpanPlan p;
   p.sbase = staged ? sbase : safe;
   p.nch = staged ? (uint32_t)((hi - sbase + 15) >> 4) : 0u;
-  p.n0 = 0;
-  if constexpr (kUniform) {
-    const uint32_t n0 = __builtin_amdgcn_readlane((uint32_t)n, fl);
-    const bool uniform = (__ballot(act) & __ballot((uint32_t)n != n0)) == 0ull;
-    p.n0 = staged && uniform ? n0 : 0u;
-  }
   return p;
 }
 
@@ -428,7 +399,6 @@ __device__ __forceinline__ void fetch_span(const SpanPlan& p, u32x4& c0, u32x4& 
   c1 = *reinterpret_cast<gcu32x4>(a1);
 }
 
-template <bool kUniform>
 __device__ __forceinline__ uint32_t staged_hash(uint32_t* stg, const SpanPlan& p, u32x4 c0, u32x4 c1,
                                                 uint64_t s, uint64_t n, bool act) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -436,19 +406,13 @@ __device__ __forceinline__ uint32_t staged_hash(uint32_t* stg, const SpanPlan& p
   if (lane < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * lane) = c0;
   if (lane + 64u < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * (lane + 64u)) = c1;
   wave_phase();
+  const uint64_t nz = __ballot(n > 0);
+  const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
   const uint32_t rel = act ? (uint32_t)(s - p.sbase) : 0u;
-  uint32_t n0;
-  if constexpr (kUniform) {
-    n0 = p.n0;  // (decided with the plan, a round ahead)
-  } else {
-    const uint64_t nz = __ballot(n != 0);
-    const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
-    n0 = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane((uint32_t)n, fl));
-    if ((__ballot(act) & __ballot((uint32_t)n != n0)) != 0ull) n0 = 0;
-  }
+  const uint32_t n0 = (uint32_t)readlane64(n, fl);
   uint32_t h;
-  if (n0 != 0)
-    h = hash_key_lds_uniform(stg, rel, n0, kBloomSeed);
+  if (__ballot(act && n != n0) == 0ull)
+    h = hash_key_lds_uniform(stg, rel, __builtin_amdgcn_readfirstlane(n0), kBloomSeed);
   else
     h = hash_key_lds(stg, rel, (uint32_t)n, kBloomSeed);
   wave_phase();  // (the next round's staging writes after these reads)
@@ -530,9 +494,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
   // 0.354 -> 0.348 ms, profiles/r02/bloom/ab_slots.log.)
   __shared__ __attribute__((aligned(16))) uint4 slots[kBloomWaves][kBloomGroup];
   __shared__ uint32_t slot_c32[kBloomWaves][kBloomGroup];
-  __shared__ float slot_rcp[kBloomWaves][kBloomGroup];  // 1 / d, correctly rounded (fmod_f32)
-  static_assert(LSBM_BUILD_WAVES_PER_EU * (sizeof(lds) + sizeof(slots) + sizeof(slot_c32) + sizeof(slot_rcp)) <=
-                    160u * 1024u,
+  static_assert(LSBM_BUILD_WAVES_PER_EU * (sizeof(lds) + sizeof(slots) + sizeof(slot_c32)) <= 160u * 1024u,
                 "the build grid's workgroups per CU must fit one CU's LDS");
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -622,11 +584,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
       // less: 0.300 -> 0.295-0.298 ms, profiles/r04/check11/build_*.log)
       slots[wv][lane] = make_uint4(8u * (lds_addr(bm) + byte_t), d_t, (uint32_t)m_t, (uint32_t)(m_t >> 32));
       slot_c32[wv][lane] = c == d_t ? 0u : c;
-      slot_rcp[wv][lane] = 1.0f / (float)d_t;
     }
-    // every filter of the group in fmod_f32's range: its remainders in single
-    // precision (db_bench's 84-byte filters: d = 672)
-    const bool fdiv = __ballot(lane < g && (bytes * 8 <= 640u || bytes * 8 >= (1u << 24))) == 0ull;
     const uint32_t st_t = lane < g ? (uint32_t)(k0 - kb0) : 0xffffffffu;
     for (uint32_t i = lane; i < (uint32_t)total; i += 64) bm[i] = 0;
     wave_phase();
@@ -643,7 +601,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
     {
       const bool act = lane < nkeys;
       const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
-      plan = plan_span<true>(kbase + oa0, n, avail, safe, act);
+      plan = plan_span(kbase + oa0, n, avail, safe);
       fetch_span(plan, ch0, ch1);
     }
 #if LSBM_BUILD_DEPTH == 2
@@ -655,7 +613,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
     {
       const bool act1 = lane + 64u < nkeys;
       const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-      plan2 = plan_span<true>(kbase + ob0, n1, avail, safe, act1);
+      plan2 = plan_span(kbase + ob0, n1, avail, safe);
       fetch_span(plan2, ch2, ch3);
     }
 #endif
@@ -668,17 +626,16 @@ void bloom_build_kernel(BloomBuildArgs a) {
       // or before r -- a wave-uniform handful (~2 of 33-key filters per
       // 64-key round), each read with readlane.  (Round 3: a 5-step binary
       // search, a chain of dependent ds_bpermute round trips every round.)
-      // (st_t is ~0 in the lanes past the group's filters: one compare each)
-      const uint32_t c0 = (uint32_t)__builtin_popcountll(__ballot(st_t < r0));
-      const uint32_t c1 = (uint32_t)__builtin_popcountll(__ballot(st_t < r0 + 64u));
+      const uint32_t c0 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0));
+      const uint32_t c1 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0 + 64u));
       uint32_t cnt = c0;
       for (uint32_t q = c0; q < c1; q++)
         cnt += (uint32_t)__builtin_amdgcn_readlane((int)st_t, (int)q) <= r ? 1u : 0u;
       const uint32_t j = cnt - 1u;  // (filter 0 starts at key 0: cnt >= 1)
       const uint4 sl = slots[wv][j];
       const uint32_t bbase = sl.x, d = sl.y;
+      const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;
       const uint32_t c32 = slot_c32[wv][j];
-      const float rcp = slot_rcp[wv][j];
       const uint64_t s = kbase + oa0;
       const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
       // this round's chunks into LDS, then the next round's plan and loads
@@ -691,7 +648,7 @@ void bloom_build_kernel(BloomBuildArgs a) {
       {
         const bool act2 = r + 128u < nkeys;
         const uint64_t n2 = act2 && oc1 >= oc0 + a.strip ? oc1 - oc0 - a.strip : 0;
-        plan2 = plan_span<true>(kbase + oc0, n2, avail, safe, act2);
+        plan2 = plan_span(kbase + oc0, n2, avail, safe);
         fetch_span(plan2, ch2, ch3);
         oa0 = ob0;
         oa1 = ob1;
@@ -703,26 +660,17 @@ void bloom_build_kernel(BloomBuildArgs a) {
       {
         const bool act1 = r + 64u < nkeys;
         const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-        plan = plan_span<true>(kbase + ob0, n1, avail, safe, act1);
+        plan = plan_span(kbase + ob0, n1, avail, safe);
         fetch_span(plan, ch0, ch1);
         oa0 = ob0;
         oa1 = ob1;
         if (r + 128u < nkeys) load_off2(ko, r + 128, ob0, ob1);
       }
 #endif
-      const uint32_t h = staged_hash<true>(stg, cur, cc0, cc1, s, n, act);
+      const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
       if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
-      uint32_t hm, dm;
-      if (fdiv) {
-        hm = fmod_f32(h, rcp, d);
-        dm = fmod_f32(delta, rcp, d);
-      } else {
-        const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;
-        hm = fastmod(h, M, d);
-        dm = fastmod(delta, M, d);
-      }
-      ProbeSeq ps = probe_seq(h, delta, hm, dm, c32, d);
+      ProbeSeq ps = probe_seq(h, delta, fastmod(h, M, d), fastmod(delta, M, d), c32, d);
 #ifdef LSBM_PROBE_UNROLL  // A/B builds only
 #pragma unroll LSBM_PROBE_UNROLL
 #endif
@@ -879,7 +827,7 @@ void bloom_probe_kernel(BloomProbeArgs a) {
   {
     const bool act = q00 + lane < a.n;
     const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
-    plan = plan_span<false>(kbase + oa0, n, avail, safe, act);
+    plan = plan_span(kbase + oa0, n, avail, safe);
     fetch_span(plan, ch0, ch1);
   }
   for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
@@ -899,13 +847,13 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     {
       const bool act1 = q + stride < a.n;
       const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-      plan = plan_span<false>(kbase + ob0, n1, avail, safe, act1);
+      plan = plan_span(kbase + ob0, n1, avail, safe);
       fetch_span(plan, ch0, ch1);
       oa0 = ob0;
       oa1 = ob1;
       if (q + 2 * stride < a.n) load_off2(a.key_offsets, q + 2 * stride, ob0, ob1);
     }
-    const uint32_t h = staged_hash<false>(stg, cur, cc0, cc1, ks, kn, act);
+    const uint32_t h = staged_hash(stg, cur, cc0, cc1, ks, kn, act);
     if (!act) continue;
 #else
   for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q0 < a.n; q0 += stride) {

@@ -19,7 +19,7 @@ constexpr int kBloomThreads = 256;                 // 4 waves per workgroup
 constexpr int kBloomWaves = kBloomThreads / 64;
 constexpr uint32_t kBloomWindowBytes = 4096;       // filter bytes a wave holds in LDS at once (build_one)
 constexpr uint32_t kBloomWindowWords = kBloomWindowBytes / 4;
-constexpr uint32_t kBloomRegionWords = 1248;       // a wave's LDS: a packed group's filters + key staging
+constexpr uint32_t kBloomRegionWords = 1280;       // a wave's LDS: a packed group's filters + key staging
 constexpr uint32_t kBloomGroup = 32;                // filters a wave takes at a time (<= 64)
 static_assert(kBloomRegionWords >= kBloomWindowWords + 1, "build_one's window + pad word");
 

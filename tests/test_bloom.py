@@ -287,65 +287,6 @@ def gpu_build(torch, keys, filters, bits_per_key, strip=0, gap=0):
     return out.cpu().numpy(), offs, sizes
 
 
-def fmod_f32(n, d):
-    """bloom_kernels.hip fmod_f32, restated in numpy float32 (IEEE single:
-    uint32 -> float32 rounds to nearest, the reciprocal is correctly rounded,
-    the product rounds once, the conversion back truncates)."""
-    n = np.asarray(n, dtype=np.uint32)
-    d32 = np.uint32(d)
-    rcp = np.float32(1.0) / np.float32(d)
-    q = (n.astype(np.float32) * rcp).astype(np.uint32)
-    prod = ((q.astype(np.uint64) & 0xFFFFFF) * (int(d) & 0xFFFFFF)) & 0xFFFFFFFF  # __umul24
-    r = (n.astype(np.uint64) - prod) & 0xFFFFFFFF
-    r = r.astype(np.uint32)
-    with np.errstate(over="ignore"):
-        r = np.minimum(r, r + d32)
-        r = np.minimum(r, r - d32)
-    return r
-
-
-def test_fmod_f32_arithmetic():
-    """The build kernel's single-precision remainder is exact for every
-    640 < d < 2^24 it is used with (d a multiple of 8: filter bytes * 8):
-    sampled d, with n at random and at the edges where the quotient estimate
-    is one off (multiples of d and their neighbours, values near 2^32)."""
-    rng = np.random.default_rng(20261017)
-    ds = np.concatenate([[648, 656, 672, 680, 1024, 4096, (1 << 24) - 8],
-                         rng.integers(81, (1 << 21), size=300) * 8]).astype(np.int64)
-    for d in ds:
-        d = int(d)
-        n = rng.integers(0, 1 << 32, size=20000, dtype=np.uint64)
-        k = rng.integers(0, (1 << 32) // d, size=4000, dtype=np.uint64)
-        edge = np.concatenate([k * d, k * d + 1, k * d - 1, k * d + d - 1,
-                               np.arange((1 << 32) - 4096, 1 << 32, dtype=np.uint64),
-                               np.arange(0, 4096, dtype=np.uint64)])
-        n = np.concatenate([n, edge[(edge < (1 << 32))]]).astype(np.uint32)
-        assert np.array_equal(fmod_f32(n, d), n % np.uint32(d)), d
-
-
-@pytest.mark.gpu
-def test_gpu_build_single_precision_remainders(torch_cuda, bloom_oracle):
-    """Groups whose 32 filters all have 640 < bits < 2^24 take the build's
-    single-precision remainders (fmod_f32): bit-exact with the oracle from
-    the smallest such filter (648 bits) up, db_bench's 672-bit filters among
-    them."""
-    torch = torch_cuda
-    rng = np.random.default_rng(648)
-    counts = rng.integers(33, 200, size=3000)
-    counts[::7] = 33  # 20 * 33 = 660 bits -> 83 bytes -> 664
-    counts[1::7] = 34  # 680 bits
-    keys = random_keys(6480, int(counts.sum()), 8, 40)
-    filters, k = [], 0
-    for c in counts:
-        filters.append((k, k + int(c)))
-        k += int(c)
-    out, offs, sizes = gpu_build(torch, keys, filters, 20, 8, 0)
-    bad = [i for i, (k0, k1) in enumerate(filters)
-           if out[int(offs[i]):int(offs[i]) + sizes[i]].tobytes()
-           != bloom_oracle.create_filter(take(keys, range(k0, k1)), 20, 8)]
-    assert bad == []
-
-
 @pytest.mark.gpu
 def test_gpu_build_groups_that_fill_the_lds_region(torch_cuda, bloom_oracle):
     """Groups of 32 filters whose bit arrays (nearly) fill a wave's LDS region
