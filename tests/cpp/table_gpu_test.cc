@@ -131,6 +131,59 @@ int main() {
   EXPECT(nbad == 1 && oks[base9 + 4] == 0);
   if (reg) (void)hipHostUnregister(&files[7][0]);
 
+  // ---- a small page-locked job (every image registered, <= 64 MiB): each
+  // table one whole-image DMA and one kernel (or, LSBM_SMALL_LOCKED=zc, read
+  // in place), tables spread over the stages: 6 tables, one empty, one with
+  // its handles out of order, more tables than stages ----
+  {
+    const size_t st_n = 6;
+    std::vector<std::string> f(st_n);
+    std::vector<std::vector<lsbm::BlockHandle>> h(st_n);
+    std::vector<std::vector<uint8_t>> y(st_n);
+    std::vector<lsbm::TableImage> ti(st_n);
+    std::vector<bool> regd(st_n, false);
+    for (size_t t = 0; t < st_n; t++) {
+      const size_t nb = t == 2 ? 0 : 200 + rng() % 1200;
+      std::vector<uint64_t> sz(nb);
+      for (auto& x : sz) x = rng() % 4 == 0 ? rng() % 100 : 3500 + rng() % 1200;
+      uint64_t fs = 0;
+      h[t] = lsbm::LayoutBlocks(sz, &fs);
+      f[t].assign(fs + 3, '\0');
+      for (auto& c : f[t]) c = (char)(' ' + rng() % 95);
+      y[t].resize(nb);
+      for (auto& x : y[t]) x = rng() % 3;
+      if (t == 4) std::reverse(h[t].begin(), h[t].end());
+      ti[t] = lsbm::TableImage{&f[t][0], f[t].size(), h[t].data(), y[t].data(), nb};
+      regd[t] = hipHostRegister(&f[t][0], f[t].size(), hipHostRegisterDefault) == hipSuccess;
+      EXPECT(regd[t]);
+    }
+    st = lsbm::SealTables(0, ti.data(), st_n);
+    EXPECT(st.ok());
+    size_t nblk = 0;
+    for (size_t t = 0; t < st_n; t++)
+      for (size_t i = 0; i < h[t].size(); i++, nblk++) {
+        const char* block = f[t].data() + h[t][i].offset;
+        char trailer[5];
+        trailer[0] = (char)y[t][i];
+        uint32_t crc = leveldb::crc32c::Extend(leveldb::crc32c::Value(block, h[t][i].size), trailer, 1);
+        encode_fixed32(trailer + 1, leveldb::crc32c::Mask(crc));
+        EXPECT(memcmp(trailer, block + h[t][i].size, 5) == 0);
+      }
+    std::vector<uint8_t> ok2;
+    st = lsbm::VerifyTables(0, ti.data(), st_n, &ok2);
+    EXPECT(st.ok() && ok2.size() == nblk && std::count(ok2.begin(), ok2.end(), 1) == (long)nblk);
+    f[5][h[5][7].offset + h[5][7].size + 2] ^= 0x40;  // a stored crc byte of table 5, block 7
+    st = lsbm::VerifyTables(0, ti.data(), st_n, &ok2);
+    size_t base5 = 0;
+    for (size_t t = 0; t < 5; t++) base5 += h[t].size();
+    EXPECT(st.IsCorruption() && std::count(ok2.begin(), ok2.end(), 0) == 1 && ok2[base5 + 7] == 0);
+    std::vector<uint8_t> ok1;  // one table per call, as TableBuilder::Finish
+    st = lsbm::VerifyBlocks(0, f[1].data(), f[1].size(), h[1].data(), h[1].size(), &ok1);
+    EXPECT(st.ok() && std::count(ok1.begin(), ok1.end(), 1) == (long)h[1].size());
+    for (size_t t = 0; t < st_n; t++)
+      if (regd[t]) (void)hipHostUnregister(&f[t][0]);
+  }
+
   // ---- error paths: a pipeline that fails with chunks in flight ----
   // (lsbm_test_fail_host_pipeline: the failure a copy or launch error would
   // give, after two chunks were enqueued).  The next call must neither collect

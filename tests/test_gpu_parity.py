@@ -406,8 +406,10 @@ def test_config3_full_1M_x_64KiB(torch_cuda, oracle, golden):
 
 
 # ---------------------------------------------------------------- C++ host layer
-def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
-    """include/lsbm/table_checksum.h used from C++ the way table/ would."""
+@pytest.mark.parametrize("small", ["", "zc"], ids=["small-locked-dma", "small-locked-zero-copy"])
+def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path, small):
+    """include/lsbm/table_checksum.h used from C++ the way table/ would; its
+    small page-locked jobs both ways (whole-image DMA, or LSBM_SMALL_LOCKED=zc)."""
     import os
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -418,7 +420,10 @@ def test_cpp_table_layer_seal_verify(torch_cuda, tmp_path):
                     os.path.join(repo, "tests", "cpp", "table_gpu_test.cc"), "-L", libdir,
                     "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
                     "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ)
+    if small:
+        env["LSBM_SMALL_LOCKED"] = small
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")
 
