@@ -336,6 +336,39 @@ void parallel_copy(void* dst, const void* src, size_t n) {
   });
 }
 
+// ---- per-call page locks ----
+bool CallLocks::enabled() {
+  static const bool on = [] {
+    const char* e = getenv("LSBM_AUTO_LOCK");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+bool CallLocks::add(int device, const void* p, size_t n, bool writable) {
+  static int read_only[kMaxDevices];  // 0 unknown, 1 supported, 2 not
+  if (!p || n == 0 || device < 0 || device >= kMaxDevices) return false;
+  if (__atomic_load_n(&read_only[device], __ATOMIC_RELAXED) == 0) {
+    hipDeviceProp_t prop;
+    const int v = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.hostRegisterReadOnlySupported ? 1 : 2;
+    __atomic_store_n(&read_only[device], v, __ATOMIC_RELAXED);
+  }
+  const bool ro = __atomic_load_n(&read_only[device], __ATOMIC_RELAXED) == 1;
+  if (!ro && !writable) return false;
+  void* q = const_cast<void*>(p);
+  if (hipHostRegister(q, n, ro ? hipHostRegisterReadOnly : hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  regs_.push_back(q);
+  return true;
+}
+
+CallLocks::~CallLocks() {
+  for (void* q : regs_) (void)hipHostUnregister(q);
+  if (!regs_.empty()) (void)hipGetLastError();
+}
+
 // ---- buffers ----
 // Page-locked host memory on `node` (the device's NUMA node): the pages are
 // placed by the allocating thread's policy (hipHostMallocNumaUser) set to

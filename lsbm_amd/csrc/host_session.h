@@ -179,6 +179,29 @@ int session_count(int device);
 // Is [p, p + n) inside page-locked host memory (hipHostMalloc'd or registered)?
 bool host_pinned(const void* p, size_t n);
 
+// Page-locks a call's pageable images (hipHostRegister: ~1 us, the pages are
+// pinned by the DMA that reads them) so that they are DMA-ed in place with no
+// staging copy, and unlocks them when destroyed.  Declare it BEFORE the
+// call's SessionLease: the lease, destroyed first, has synchronised every
+// stream that may still read an image.  The device only reads the images
+// (hipHostRegisterReadOnly where the device supports it, so read-only
+// mappings such as an mmap'd table file qualify; else only images the caller
+// passed as writable).  LSBM_AUTO_LOCK=0 turns it off (staging copies).
+class CallLocks {
+ public:
+  CallLocks() = default;
+  CallLocks(const CallLocks&) = delete;
+  CallLocks& operator=(const CallLocks&) = delete;
+  ~CallLocks();
+  // true when [p, p + n) is page-locked for this call from here on (false: it
+  // could not be, e.g. a page of it is registered already; nothing changed)
+  bool add(int device, const void* p, size_t n, bool writable);
+  static bool enabled();
+
+ private:
+  std::vector<void*> regs_;
+};
+
 // fn(0) ... fn(pieces - 1) over the worker pool and the caller; returns when
 // all have run.  The pool has usable_cores() - 1 threads (the affinity mask
 // capped by the cgroup CPU quota), grouped by NUMA node; jobs of concurrent

@@ -71,15 +71,29 @@ struct Plan {
 
 // Whole blocks (and trailers) in offset order, packed into chunks of at most
 // HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own),
-// closed once they reach an equal share of the bytes: no runt chunk at the
+// closed once they reach their share of the bytes: no runt chunk at the
 // end (a 1-block fifth chunk cost a kernel launch and a blit per 16 MiB
 // table, profiles/r04/one_table_trace/summary_call40.txt).
 void make_plan(const TableImage* tables, size_t count, Plan* p) {
   p->order.resize(count);
   size_t total = 0;
   for (size_t t = 0; t < count; t++) total += tables[t].file_size;
-  const size_t limit = HostSession::chunk_for(total);
-  const size_t target = total / std::max<size_t>(1, (total + limit - 1) / limit);
+  size_t limit = HostSession::chunk_for(total);
+  const size_t nch = std::max<size_t>(1, (total + limit - 1) / limit);
+  size_t target = total / nch, first = target;
+  // A job of at most kStages chunks (one table per call) has all of them in
+  // flight at once, and the first chunk's staging copy is its lead time
+  // before any DMA starts: a short first chunk (1/16 of a 16 MiB table), the
+  // rest in equal shares.  LSBM_CHUNK_RAMP=0: equal chunks (A/B).
+  static const bool ramp = [] {
+    const char* e = getenv("LSBM_CHUNK_RAMP");
+    return !e || atoi(e) != 0;
+  }();
+  if (ramp && nch > 1 && nch <= (size_t)HostSession::kStages) {
+    first = std::max<size_t>(256u << 10, total / (4 * nch));
+    target = (total - std::min(total, first) + nch - 2) / (nch - 1);
+    limit = std::max(limit, target);
+  }
   Chunk cur;
   auto close = [&]() {
     if (cur.blocks == 0) return;
@@ -106,7 +120,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
       if (open) {
         Piece& pc = cur.pieces.back();
         const uint64_t hi = std::max(pc.hi, end);
-        if (cur.bytes < target && cur.bytes + (hi - pc.hi) <= limit) {
+        if (cur.bytes < (p->chunks.empty() ? first : target) && cur.bytes + (hi - pc.hi) <= limit) {
           cur.bytes += hi - pc.hi;
           pc.hi = hi;
           pc.count++;
@@ -115,7 +129,8 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
         }
         close();
       }
-      if (cur.blocks && (cur.bytes >= target || cur.bytes + (end - h.offset) > limit)) close();
+      if (cur.blocks && (cur.bytes >= (p->chunks.empty() ? first : target) || cur.bytes + (end - h.offset) > limit))
+        close();
       cur.pieces.push_back(Piece{(uint32_t)t, h.offset, end, k, 1, cur.bytes});
       cur.bytes += end - h.offset;
       cur.blocks++;
@@ -274,16 +289,27 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
   std::vector<uint8_t> pinned(count);
   for (size_t t = 0; t < count; t++) pinned[t] = host_pinned(tables[t].file, tables[t].file_size);
 
+  CallLocks locks;  // (before the lease: unlocked after its streams are synchronised)
   SessionLease s;
   Status st = s.Open(device);
   if (!st.ok()) return st;
   {
     size_t total = 0;
+    for (size_t t = 0; t < count; t++) total += tables[t].file_size;
+    // A small job's pageable images are page-locked for the call and DMA-ed
+    // in place: one 16 MiB table per call 0.355 ms, registration included,
+    // against 0.39-0.60 ms through the staging copy, box to box
+    // (profiles/r04/check17/, seal_register_per_call vs seal_pageable).
+    // Big jobs keep the staging pipeline (53.8 against 51.3 GB/s in place,
+    // profiles/r04/check13/host_*.log).
+    // (not for zero copy: its seal stores into the image, and a read-only
+    // registration must never be written by the device)
+    if (total <= zero_copy_max() && CallLocks::enabled() && !small_locked_zero_copy())
+      for (size_t t = 0; t < count; t++)
+        if (!pinned[t] && tables[t].n != 0)
+          pinned[t] = locks.add(device, tables[t].file, tables[t].file_size, op == Op::kSeal);
     bool all_pinned = true;
-    for (size_t t = 0; t < count; t++) {
-      total += tables[t].file_size;
-      all_pinned = all_pinned && (tables[t].n == 0 || pinned[t]);
-    }
+    for (size_t t = 0; t < count; t++) all_pinned = all_pinned && (tables[t].n == 0 || pinned[t]);
     if (all_pinned && total <= zero_copy_max() &&
         run_small_locked(*s, tables, count, op, ok_out, ok_base, nbad_out, tm, &st))
       return st;  // (false: zero copy asked for and an image without a device mapping)

@@ -4,6 +4,8 @@
 // (table/format.cc:95-103), computed with util/crc32c.h.  Needs a GPU.
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <random>
@@ -182,6 +184,30 @@ int main() {
     EXPECT(st.ok() && std::count(ok1.begin(), ok1.end(), 1) == (long)h[1].size());
     for (size_t t = 0; t < st_n; t++)
       if (regd[t]) (void)hipHostUnregister(&f[t][0]);
+
+    // the sealed table read back through a read-only mapping of its file, as
+    // the reference's PosixMmapReadableFile hands ReadBlock its bytes: the
+    // layer may page-lock it for the call (read-only) or stage it; either
+    // way every block verifies, and one flipped byte is found
+    char path[] = "/tmp/lsbm_table_XXXXXX";
+    const int fd = mkstemp(path);
+    EXPECT(fd >= 0);
+    if (fd >= 0) {
+      f[1][h[1][3].offset + 1] ^= 0x01;  // block 3 of the file copy is corrupt
+      EXPECT(write(fd, f[1].data(), f[1].size()) == (ssize_t)f[1].size());
+      f[1][h[1][3].offset + 1] ^= 0x01;
+      void* m = mmap(nullptr, f[1].size(), PROT_READ, MAP_PRIVATE, fd, 0);
+      EXPECT(m != MAP_FAILED);
+      if (m != MAP_FAILED) {
+        for (int rep = 0; rep < 2; rep++) {  // (a second call: the lock was released)
+          st = lsbm::VerifyBlocks(0, static_cast<const char*>(m), f[1].size(), h[1].data(), h[1].size(), &ok1);
+          EXPECT(st.IsCorruption() && std::count(ok1.begin(), ok1.end(), 0) == 1 && ok1[3] == 0);
+        }
+        munmap(m, f[1].size());
+      }
+      close(fd);
+      unlink(path);
+    }
   }
 
   // ---- error paths: a pipeline that fails with chunks in flight ----

@@ -7,9 +7,13 @@
 // p99 / max / mean, the slowest calls' indices) and the cgroup CPU throttling
 // counters (/sys/fs/cgroup/cpu.stat: nr_periods, nr_throttled,
 // throttled_usec) read before and after the phase:
+//   host_copy_*                           the pageable layers' staging copy alone
 //   seal_pageable, verify_pageable        reps calls each, back to back
 //   alternate_pageable                    seal, verify, seal, ... (reps each)
+//   seal_register_per_call                hipHostRegister + seal + unregister
 //   seal_locked, verify_locked            the same image hipHostRegister'ed
+//   zerocopy_*, dma_*                     the device ABI on the registered image
+//                                         in place, and the DMA path's floor
 //   concurrent_seal                       C caller threads, each sealing its
 //                                         own table reps / C times, against the
 //                                         same calls made one after another
@@ -20,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -229,6 +234,48 @@ int main(int argc, char** argv) {
       print_phase("alternate_seal_pageable", vs, bytes, a, b, s.ToString().c_str(), check_table(t));
       print_phase("alternate_verify_pageable", vv, bytes, a, b, s.ToString().c_str(), 0);
       if (!s.ok()) return 1;
+    }
+    if (!locked) {
+      // page-locking the image for each call (hipHostRegister, seal,
+      // hipHostUnregister): what a caller that does not keep its write buffer
+      // registered would pay; and the registration alone, on this image
+      // (std::vector: transparent huge pages where the system gives them) and
+      // on a copy in 4 KiB pages (MADV_NOHUGEPAGE)
+      auto reg_seal = [&](Table& tb) {
+        if (hipHostRegister(tb.img.data(), tb.img.size(), hipHostRegisterDefault) != hipSuccess)
+          return lsbm::Status::IOError("hipHostRegister");
+        lsbm::Status r = seal(tb);
+        (void)hipHostUnregister(tb.img.data());
+        return r;
+      };
+      auto reg_only = [&](void* p, size_t n) {
+        if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) return lsbm::Status::IOError("register");
+        return hipHostUnregister(p) == hipSuccess ? lsbm::Status::OK() : lsbm::Status::IOError("unregister");
+      };
+      if (!phase("seal_register_per_call", [&] { return reg_seal(t); })) return 1;
+      if (!phase("register_unregister_only", [&] { return reg_only(t.img.data(), t.img.size()); })) return 1;
+      const size_t n4 = (t.img.size() + 4095) & ~(size_t)4095;
+      void* m4 = mmap(nullptr, n4, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m4 != MAP_FAILED) {
+        (void)madvise(m4, n4, MADV_NOHUGEPAGE);
+        memcpy(m4, t.img.data(), t.img.size());
+        if (!phase("register_unregister_only_4k_pages", [&] { return reg_only(m4, t.img.size()); })) return 1;
+        if (!phase("seal_register_per_call_4k_pages", [&] {
+              if (hipHostRegister(m4, t.img.size(), hipHostRegisterDefault) != hipSuccess)
+                return lsbm::Status::IOError("hipHostRegister");
+              lsbm::Status r = lsbm::SealBlocks(0, static_cast<char*>(m4), t.img.size(), t.h.data(), t.types.data(),
+                                                t.h.size());
+              (void)hipHostUnregister(m4);
+              return r;
+            }))
+          return 1;
+        if (!phase("seal_pageable_4k_pages", [&] {
+              return lsbm::SealBlocks(0, static_cast<char*>(m4), t.img.size(), t.h.data(), t.types.data(),
+                                      t.h.size());
+            }))
+          return 1;
+        munmap(m4, n4);
+      }
     }
     if (locked) {
       // Zero-copy experiment: the device ABI's kernels reading the registered
