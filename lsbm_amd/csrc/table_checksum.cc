@@ -224,12 +224,17 @@ bool run_small_locked(HostSession& hs, const TableImage* tables, size_t count, O
     return Status::OK();
   };
   int k = 0;
+  size_t enq = 0;
   for (size_t t = 0; t < count; t++) {
     const TableImage& tb = tables[t];
     if (tb.n == 0) continue;
     Stage& sg = hs.stage(k);
     k = (k + 1) % HostSession::kStages;
     if (sg.busy && !(*st = collect(sg)).ok()) return true;
+    if (host_fault_point(enq++)) {  // (tests: a failure with tables in flight)
+      *st = Status::IOError("injected fault");
+      return true;
+    }
     hipError_t e = sg.zmeta.reserve_mapped(tb.n * (sizeof(BlockHandle) + 1) + 16);
     if (e == hipSuccess) e = sg.res.reserve_mapped(tb.n * 4 + 16);
     if (e == hipSuccess && !zc) e = sg.bulk.reserve(tb.file_size + 64);  // (+ the kernel's row slack)

@@ -216,8 +216,14 @@ int main(int argc, char** argv) {
       return 1;
     }
     const std::string sfx = locked ? "_locked" : "_pageable";
-    if (!phase(("seal" + sfx).c_str(), [&] { return seal(t); })) return 1;
-    if (!phase(("verify" + sfx).c_str(), [&] { return verify(t); })) return 1;
+    if (getenv("LSBM_BENCH_VERIFY_FIRST")) {  // (order effects: verify, seal, verify again)
+      if (!phase(("verify" + sfx).c_str(), [&] { return verify(t); })) return 1;
+      if (!phase(("seal" + sfx).c_str(), [&] { return seal(t); })) return 1;
+      if (!phase(("verify_again" + sfx).c_str(), [&] { return verify(t); })) return 1;
+    } else {
+      if (!phase(("seal" + sfx).c_str(), [&] { return seal(t); })) return 1;
+      if (!phase(("verify" + sfx).c_str(), [&] { return verify(t); })) return 1;
+    }
     if (!locked) {
       // seal and verify alternating: is the seal's tail the order it runs in?
       std::vector<double> vs, vv;
