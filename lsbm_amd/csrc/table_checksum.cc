@@ -71,29 +71,18 @@ struct Plan {
 
 // Whole blocks (and trailers) in offset order, packed into chunks of at most
 // HostSession::chunk_for(all bytes) (a larger block gets a chunk of its own),
-// closed once they reach their share of the bytes: no runt chunk at the
+// closed once they reach an equal share of the bytes: no runt chunk at the
 // end (a 1-block fifth chunk cost a kernel launch and a blit per 16 MiB
 // table, profiles/r04/one_table_trace/summary_call40.txt).
 void make_plan(const TableImage* tables, size_t count, Plan* p) {
   p->order.resize(count);
   size_t total = 0;
   for (size_t t = 0; t < count; t++) total += tables[t].file_size;
-  size_t limit = HostSession::chunk_for(total);
-  const size_t nch = std::max<size_t>(1, (total + limit - 1) / limit);
-  size_t target = total / nch, first = target;
-  // A job of at most kStages chunks (one table per call) has all of them in
-  // flight at once, and the first chunk's staging copy is its lead time
-  // before any DMA starts: a short first chunk (1/16 of a 16 MiB table), the
-  // rest in equal shares.  LSBM_CHUNK_RAMP=0: equal chunks (A/B).
-  static const bool ramp = [] {
-    const char* e = getenv("LSBM_CHUNK_RAMP");
-    return !e || atoi(e) != 0;
-  }();
-  if (ramp && nch > 1 && nch <= (size_t)HostSession::kStages) {
-    first = std::max<size_t>(256u << 10, total / (4 * nch));
-    target = (total - std::min(total, first) + nch - 2) / (nch - 1);
-    limit = std::max(limit, target);
-  }
+  const size_t limit = HostSession::chunk_for(total);
+  const size_t target = total / std::max<size_t>(1, (total + limit - 1) / limit);
+  // (A short first chunk, to shorten the staging copy's lead before the
+  // first DMA, measured no different: 0.401-0.411 against 0.403-0.413 ms per
+  // 16 MiB table, profiles/r04/check16/.)
   Chunk cur;
   auto close = [&]() {
     if (cur.blocks == 0) return;
@@ -120,7 +109,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
       if (open) {
         Piece& pc = cur.pieces.back();
         const uint64_t hi = std::max(pc.hi, end);
-        if (cur.bytes < (p->chunks.empty() ? first : target) && cur.bytes + (hi - pc.hi) <= limit) {
+        if (cur.bytes < target && cur.bytes + (hi - pc.hi) <= limit) {
           cur.bytes += hi - pc.hi;
           pc.hi = hi;
           pc.count++;
@@ -129,8 +118,7 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
         }
         close();
       }
-      if (cur.blocks && (cur.bytes >= (p->chunks.empty() ? first : target) || cur.bytes + (end - h.offset) > limit))
-        close();
+      if (cur.blocks && (cur.bytes >= target || cur.bytes + (end - h.offset) > limit)) close();
       cur.pieces.push_back(Piece{(uint32_t)t, h.offset, end, k, 1, cur.bytes});
       cur.bytes += end - h.offset;
       cur.blocks++;
