@@ -8,11 +8,14 @@
 // into the host image by the host) or 1 B (verify: the ok flag) per block
 // return to the host, never the image.
 //
-// One 16 MiB table per call (TableBuilder::Finish, lsbm/db_impl.cc:843-892)
-// is four 4 MiB chunks, one per stage, so no chunk waits for a stage to come
-// free.  A pageable chunk's handles and types travel in its staging buffer
-// behind its bytes (one DMA per chunk); a page-locked chunk's metadata is
-// sent first, so that its kernel follows its bytes' DMA directly.
+// A small job -- one 16 MiB table per call, as TableBuilder::Finish makes
+// them (lsbm/db_impl.cc:843-892) -- whose images are page-locked (by the
+// caller, or by the seal for the call: CallLocks) skips the chunks: each
+// table is one whole-image DMA and one kernel on a stage's stream
+// (run_small_locked).  Otherwise one 16 MiB table is four 4 MiB chunks, one
+// per stage; a pageable chunk's handles and types travel in its staging
+// buffer behind its bytes (one DMA per chunk), a page-locked chunk's bytes
+// are DMA-ed from the image on the session's copy stream.
 #include "../../include/lsbm/table_checksum.h"
 
 #include <hip/hip_runtime_api.h>
