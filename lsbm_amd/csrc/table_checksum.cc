@@ -413,17 +413,22 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
     sg.settled = false;  // (from here on the stage's stream may hold work)
     if (direct) {
       // page-locked: the metadata first, then the bytes DMA-ed in place, on
-      // the session's copy stream (the chunks' DMAs back to back); the stage's
-      // kernel waits for this chunk's
-      hipStream_t cs = nullptr;
-      e = s->copy_stream(&cs);
+      // the stage's own stream (the stages' DMAs run side by side, as the
+      // staged path's do: a 1000-table compaction's verify 53.6 against
+      // 51.7 GB/s, seal 50.0-51.2 against 51.7, profiles/r04/check20/; one
+      // table per call takes run_small_locked).  LSBM_DIRECT_COPY_STREAM=1
+      // (A/B): on the session's copy stream, back to back, the stage's
+      // kernel waiting for its chunk.
+      static const bool copy_stream = getenv("LSBM_DIRECT_COPY_STREAM") != nullptr;
+      hipStream_t cs = sg.stream;
+      if (copy_stream) e = s->copy_stream(&cs);
       if (e == hipSuccess) e = hipMemcpyAsync(sg.meta.d, sg.meta.h, meta_n, hipMemcpyHostToDevice, cs);
       for (const Piece& pc : ch.pieces)
         if (e == hipSuccess)
           e = hipMemcpyAsync(sg.bulk.d + pc.dst, tables[pc.t].file + pc.lo, pc.hi - pc.lo,
                              hipMemcpyHostToDevice, cs);
-      if (e == hipSuccess) e = hipEventRecord(sg.copied, cs);
-      if (e == hipSuccess) e = hipStreamWaitEvent(sg.stream, sg.copied, 0);
+      if (copy_stream && e == hipSuccess) e = hipEventRecord(sg.copied, cs);
+      if (copy_stream && e == hipSuccess) e = hipStreamWaitEvent(sg.stream, sg.copied, 0);
     } else {
       // pageable: bytes and metadata through the pinned staging, one DMA
       const double t = tm.on ? HostTiming::now() : 0.0;
