@@ -84,51 +84,69 @@ struct Job {
   const std::function<void(size_t)>* fn;
   size_t pieces;
   int node;
-  std::atomic<size_t> next{0}, finished{0};
-  std::atomic<int> users{0};   // workers holding this job (picked under mu_)
-  std::atomic<int> active{0};  // pieces in progress (testing: pool_take_peak_jobs)
+  // (each counter on a cache line of its own: every thread of the job hits
+  // next once per piece, finished once per piece, and the caller polls it)
+  alignas(64) std::atomic<size_t> next{0};
+  alignas(64) std::atomic<size_t> finished{0};
+  alignas(64) std::atomic<int> active{0};  // pieces in progress (testing: pool_take_peak_jobs)
 };
 
-// Pieces are claimed and counted with atomics; mu_ guards only the job list
-// (one push and one removal per job, one pick per worker and job).  Round 4:
-// a mutex round trip per piece -- 16 threads on one std::mutex, each loser
-// parked in the kernel -- cost ~50 us per parallel_for, so a 4 MiB staging
-// copy took 64 us on 16 threads against 54 us on one
-// (profiles/r04/check11/one_table.log, host_copy_*).
+// No lock on the way to a piece.  A job is published in a slot; a worker
+// takes it with a hazard pointer (its own slot says "I may touch this job",
+// then it re-reads the job slot), claims pieces with fetch_add and counts them
+// done with another; the caller unpublishes its job, then waits until every
+// piece is done and no worker's hazard names the job.  (The hazard is stored
+// before the job slot is re-read, the job slot cleared before the hazards are
+// read, all sequentially consistent: either the worker sees its job gone, or
+// the caller sees the worker's hazard.)  The mutex is only for sleeping.
+// Round 4: with a mutex round trip per piece a parallel_for cost ~50 us; with
+// one per worker and job (pick and drop), 25-37 us of empty pieces on 16
+// threads (tools/ab/r4/pool_overhead.py) -- a 4 MiB staging copy took 0.047
+// ms where the bytes need ~0.024.
 class WorkPool {
  public:
+  static constexpr int kJobSlots = 64;
+  static constexpr int kMaxWorkers = 512;
+
   void run(size_t pieces, const std::function<void(size_t)>& fn, int node) {
+    start();
     Job j;
     j.fn = &fn;
     j.pieces = pieces;
     j.node = node;
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      start_locked();
-      jobs_.push_back(&j);
-      queued_.store(jobs_.size(), std::memory_order_release);
+    int slot = -1;
+    for (int i = 0; i < kJobSlots && slot < 0; i++) {
+      Job* e = nullptr;
+      if (jobs_[i].compare_exchange_strong(e, &j)) slot = i;
     }
-    if (pieces > 2) work_cv_.notify_all();
-    else work_cv_.notify_one();
+    if (slot >= 0) {
+      published_.fetch_add(1);
+      if (sleepers_.load() > 0) {
+        std::lock_guard<std::mutex> l(mu_);
+        work_cv_.notify_all();
+      }
+    }
     t_in_pool = true;
-    work_on(&j);  // the caller's share: pieces of its own job only
+    work_on(&j);  // the caller's share (all of it when no slot was free)
     t_in_pool = false;
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      drop_locked(&j);  // (no worker picks it up from here on)
-    }
-    // the pieces still running elsewhere, and the workers still holding j
-    for (uint32_t i = 1; j.finished.load(std::memory_order_acquire) != pieces ||
-                         j.users.load(std::memory_order_acquire) != 0;
-         i++) {
+    if (slot < 0) return;
+    jobs_[slot].store(nullptr);  // (no worker takes it from here on)
+    published_.fetch_sub(1);
+    // the pieces still running elsewhere, and the workers that may still read j
+    for (uint32_t i = 1; j.finished.load(std::memory_order_acquire) != pieces; i++) {
       _mm_pause();
       if ((i & 1023u) == 0) std::this_thread::yield();
     }
+    const int nw = nworkers_.load(std::memory_order_acquire);
+    for (int w = 0; w < nw; w++)
+      for (uint32_t i = 1; hazard_[w].load() == &j; i++) {
+        _mm_pause();
+        if ((i & 1023u) == 0) std::this_thread::yield();
+      }
   }
   int threads() {
-    std::lock_guard<std::mutex> l(mu_);
-    start_locked();
-    return (int)workers_;
+    start();
+    return nworkers_.load();
   }
   // Testing: the most jobs that had pieces running at once since the last
   // call (counted from the first call on).
@@ -154,21 +172,39 @@ class WorkPool {
       j->finished.fetch_add(1, std::memory_order_release);
     }
   }
-  void drop_locked(Job* j) {
-    auto it = std::find(jobs_.begin(), jobs_.end(), j);
-    if (it != jobs_.end()) jobs_.erase(it);
-    queued_.store(jobs_.size(), std::memory_order_release);
+  // A published job with pieces left, preferring this node's: held by hazard
+  // slot w on return (nullptr: none).
+  Job* take(int w, int node) {
+    Job* any = nullptr;
+    int any_i = -1;
+    for (int i = 0; i < kJobSlots; i++) {
+      Job* q = jobs_[i].load(std::memory_order_acquire);
+      if (!q) continue;
+      hazard_[w].store(q);
+      if (jobs_[i].load() != q || q->next.load(std::memory_order_relaxed) >= q->pieces) {
+        hazard_[w].store(nullptr);
+        continue;
+      }
+      if (q->node == node) return q;  // (held)
+      hazard_[w].store(nullptr);
+      if (!any) {
+        any = q;
+        any_i = i;
+      }
+    }
+    if (any) {  // another node's job: take it again under the hazard
+      hazard_[w].store(any);
+      if (jobs_[any_i].load() == any && any->next.load(std::memory_order_relaxed) < any->pieces) return any;
+      hazard_[w].store(nullptr);
+    }
+    return nullptr;
   }
-  Job* pick_locked(int node) {
-    for (Job* q : jobs_)
-      if (q->node == node) return q;
-    return jobs_.front();
-  }
-  void start_locked() {
-    if (started_) return;
-    started_ = true;
+  void start() {
+    if (started_.load(std::memory_order_acquire)) return;
+    std::lock_guard<std::mutex> l(mu_);
+    if (started_.load(std::memory_order_relaxed)) return;
     const std::vector<NodeCpus> nodes = process_nodes();
-    const int total = std::max(1, usable_cores() - 1);  // (the caller is the last core)
+    const int total = std::min(kMaxWorkers, std::max(1, usable_cores() - 1));  // (the caller is the last core)
     size_t cpus = 0;
     for (const NodeCpus& n : nodes) cpus += n.cpus.size();
     const bool bind = nodes.size() > 1;
@@ -181,18 +217,18 @@ class WorkPool {
                   : std::max(1, (int)((double)total * nodes[i].cpus.size() / std::max<size_t>(1, cpus) + 0.5));
       k = std::max(0, std::min(k, left));
       for (int t = 0; t < k; t++) {
-        const int node = nodes[i].node;
-        std::thread th([this, node, bind] { worker(node, bind); });
-        th.detach();  // parked on work_cv_ for the life of the process
+        const int node = nodes[i].node, w = given + t;
+        std::thread th([this, node, bind, w] { worker(w, node, bind); });
+        th.detach();  // for the life of the process
       }
       given += k;
-      workers_ += k;
     }
+    nworkers_.store(given, std::memory_order_release);
+    started_.store(true, std::memory_order_release);
   }
-  // A worker that runs out of pieces spins for spin_us() before it sleeps on
-  // work_cv_: a layer's chunks come every ~80 us, and a worker woken from
-  // sleep joins a 4 MiB staging copy late (the copy ran at ~51 GB/s on 16
-  // threads, profiles/r04/check3/timing.log).
+  // A worker that finds no job spins for spin_us() before it sleeps: a
+  // layer's chunks come every ~80 us, and a worker woken from sleep joins a
+  // 4 MiB staging copy late (profiles/r04/check3/timing.log).
   static double spin_us() {
     static const double us = [] {
       const char* v = getenv("LSBM_POOL_SPIN_US");
@@ -200,40 +236,39 @@ class WorkPool {
     }();
     return us;
   }
-  void worker(int node, bool bind) {
+  void worker(int w, int node, bool bind) {
     t_in_pool = true;
     NumaBind nb(bind ? node : -1, true, false);  // (kept bound for the thread's life)
     for (;;) {
-      if (queued_.load(std::memory_order_acquire) == 0 && spin_us() > 0) {
+      if (published_.load(std::memory_order_acquire) == 0) {
         const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t i = 1; queued_.load(std::memory_order_acquire) == 0; i++) {
+        for (uint32_t i = 1; published_.load(std::memory_order_acquire) == 0; i++) {
           _mm_pause();
           if ((i & 255u) == 0 &&
-              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us())
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us()) {
+            std::unique_lock<std::mutex> l(mu_);
+            sleepers_.fetch_add(1);
+            work_cv_.wait(l, [&] { return published_.load() > 0; });
+            sleepers_.fetch_sub(1);
             break;
+          }
         }
       }
-      Job* j;
-      {
-        std::unique_lock<std::mutex> l(mu_);
-        work_cv_.wait(l, [&] { return !jobs_.empty(); });
-        j = pick_locked(node);
-        j->users.fetch_add(1, std::memory_order_relaxed);
+      Job* j = take(w, node);
+      if (!j) {
+        _mm_pause();
+        continue;
       }
       work_on(j);
-      {
-        std::lock_guard<std::mutex> l(mu_);
-        drop_locked(j);  // (exhausted: others look elsewhere)
-      }
-      j->users.fetch_sub(1, std::memory_order_release);  // (j may be gone after this)
+      hazard_[w].store(nullptr);  // (j may be gone after this)
     }
   }
-  std::mutex mu_;
+  std::mutex mu_;  // start() and sleeping only
   std::condition_variable work_cv_;
-  std::vector<Job*> jobs_;  // jobs whose pieces may not all be claimed yet, oldest first
-  std::atomic<size_t> queued_{0};  // jobs_.size(), for the workers' spin
-  size_t workers_ = 0;
-  bool started_ = false;
+  std::atomic<Job*> jobs_[kJobSlots] = {};
+  std::atomic<Job*> hazard_[kMaxWorkers] = {};
+  std::atomic<int> published_{0}, sleepers_{0}, nworkers_{0};
+  std::atomic<bool> started_{false};
   std::atomic<int> running_{0}, active_max_{0};
   std::atomic<bool> track_{false};
 };

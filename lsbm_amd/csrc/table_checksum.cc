@@ -83,9 +83,10 @@ void make_plan(const TableImage* tables, size_t count, Plan* p) {
   for (size_t t = 0; t < count; t++) total += tables[t].file_size;
   const size_t limit = HostSession::chunk_for(total);
   const size_t target = total / std::max<size_t>(1, (total + limit - 1) / limit);
-  // (A short first chunk, to shorten the staging copy's lead before the
-  // first DMA, measured no different: 0.401-0.411 against 0.403-0.413 ms per
-  // 16 MiB table, profiles/r04/check16/.)
+  // (Unequal chunks for one table per call -- a short first one, or shares
+  // doubling from 1/15 of the job -- to shorten the staging copy's lead
+  // before the first DMA measured no different: 0.40-0.45 ms per 16 MiB table
+  // either way, profiles/r04/check16/, check21/, check22/.)
   Chunk cur;
   auto close = [&]() {
     if (cur.blocks == 0) return;
