@@ -225,6 +225,10 @@ int lsbm_test_pci_numa_node(const char* sysfs_root, const char* bus_id);
 int lsbm_test_parse_cpulist(const char* list, int* cpus, int cap);
 int lsbm_test_cgroup_quota(const char* cgroup_root);
 int lsbm_test_pool_overlap(int callers, int jobs, int pieces, int piece_us, double* seconds);
+/* Testing: `callers` threads each run `jobs` parallel jobs of 1..max_pieces
+ * pieces (some with nested jobs); returns how many pieces did not run exactly
+ * once (0 = correct), -1 for bad arguments. */
+int lsbm_test_pool_stress(int callers, int jobs, int max_pieces);
 /* Testing: 1 if the C++ layers would DMA [p, p + n) in place (page-locked by
  * hipHostMalloc or one hipHostRegister covering the whole range), else 0. */
 int lsbm_test_host_pinned(const void* p, size_t n);

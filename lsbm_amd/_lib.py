@@ -61,6 +61,7 @@ SIGNATURES = {
     "lsbm_test_pool_overlap": (_int, [_int, _int, _int, _int, _vp]),
     "lsbm_test_host_pinned": (_int, [_vp, _sz]),
     "lsbm_test_host_copy": (_int, [_vp, _vp, _sz, _int]),
+    "lsbm_test_pool_stress": (_int, [_int, _int, _int]),
     "lsbm_test_zero_copy_max_mb": (_int, [_int]),
     # include/lsbm_bloom.h
     "lsbm_bloom_hash": (_u32, [_vp, _sz, _u32]),

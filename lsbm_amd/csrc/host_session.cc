@@ -745,6 +745,38 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_overlap(int
   return lsbm::pool_take_peak_jobs();
 }
 
+// Testing: `callers` threads each run `jobs` parallel_for jobs of 1..max_pieces
+// pieces (some nested: a piece that runs its own parallel_for, inline), each
+// piece adding 1 to its own counter; returns the number of counters that
+// are not exactly 1 afterwards (0: every piece of every job ran once).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_stress(int callers, int jobs, int max_pieces) {
+  if (callers <= 0 || jobs <= 0 || max_pieces <= 0) return -1;
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int c = 0; c < callers; c++)
+    th.emplace_back([=, &bad] {
+      uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(c + 1);
+      for (int j = 0; j < jobs; j++) {
+        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+        const size_t n = 1 + (size_t)(x % (uint64_t)max_pieces);
+        std::vector<std::atomic<int>> hit(n);
+        for (auto& h : hit) h.store(0);
+        const bool nested = (x >> 40) % 5 == 0;
+        lsbm::parallel_for(n, [&](size_t k) {
+          if (nested) {
+            std::atomic<int> inner{0};
+            lsbm::parallel_for(3, [&](size_t) { inner.fetch_add(1); });
+            if (inner.load() != 3) hit[k].fetch_add(100);
+          }
+          hit[k].fetch_add(1);
+        });
+        for (auto& h : hit) bad += h.load() != 1;
+      }
+    });
+  for (auto& t : th) t.join();
+  return bad.load();
+}
+
 // Testing: host_pinned() itself (which ranges the layers DMA in place).
 extern "C" __attribute__((visibility("default"))) int lsbm_test_host_copy(void* dst, const void* src, size_t n,
                                                                       int parallel) {

@@ -111,3 +111,38 @@ def test_pool_nested_jobs_and_errors(product_lib):
     assert lib.lsbm_test_pool_overlap(0, 1, 1, 0, None) == -1
     assert lib.lsbm_test_pool_overlap(2, 3, 1, 0, None) >= 0  # one-piece jobs run inline
     assert lib.lsbm_test_pool_overlap(8, 4, 64, 50, None) >= 1
+
+
+def test_pool_every_piece_runs_once_under_contention(product_lib):
+    """The lock-free pool (job slots taken under hazard pointers, pieces
+    claimed by fetch_add): 8 callers x 400 jobs of 1-64 pieces, a fifth of
+    them running nested jobs inside their pieces -- more jobs at once than the
+    pool has threads -- and every piece of every job runs exactly once; then
+    more callers than the 64 job slots (the overflow runs inline)."""
+    lib = _lib(product_lib)
+    lib.lsbm_test_pool_stress.argtypes = [ctypes.c_int] * 3
+    assert lib.lsbm_test_pool_stress(0, 1, 1) == -1
+    assert lib.lsbm_test_pool_stress(8, 400, 64) == 0
+    assert lib.lsbm_test_pool_stress(80, 20, 16) == 0
+
+
+def test_pool_under_thread_sanitizer(tmp_path):
+    """The same stress, built with -fsanitize=thread (host code only): no data
+    race reported, every piece once (tests/cpp/pool_tsan.cc)."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(repo, "lsbm_amd", "csrc")
+    exe = tmp_path / "pool_tsan"
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-D__HIP_PLATFORM_AMD__",
+                        "-I", os.path.join(repo, "include"), "-I", "/opt/rocm/include",
+                        os.path.join(repo, "tests", "cpp", "pool_tsan.cc"), os.path.join(csrc, "host_session.cc"),
+                        os.path.join(csrc, "host_numa.cc"), os.path.join(csrc, "status.cc"),
+                        "-L", "/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath,/opt/rocm/lib",
+                        "-o", str(exe)], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("no ThreadSanitizer build here: " + r.stderr[-300:])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert r.stdout.startswith("OK"), r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
