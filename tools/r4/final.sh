@@ -3,7 +3,7 @@
 # bench; then the headline kernel's rocprofv3 stats and PMC passes
 # (tools/gpu_profile.sh) into gpurun_out/r4_final/profile.
 export TMPDIR=/tmp
-OUT=gpurun_out/r4_final
+OUT=${OUT:-gpurun_out/r4_final}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
