@@ -390,8 +390,29 @@ bool CallLocks::add(int device, const void* p, size_t n, bool writable) {
   }
   const bool ro = __atomic_load_n(&read_only[device], __ATOMIC_RELAXED) == 1;
   if (!ro && !writable) return false;
+  // Never over a registration the caller made: HIP accepts a range whose
+  // first page is registered already, and unregistering such a range can
+  // break the older one (a crash in a later call, found by table_gpu_test).
+  // Both ends must be unregistered memory; a registration strictly inside
+  // the range makes hipHostRegister fail.
+  auto registered = [](const void* x) {
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, x);
+    (void)hipGetLastError();
+    return e == hipSuccess && a.type != hipMemoryTypeUnregistered;
+  };
+  if (registered(p) || registered(static_cast<const char*>(p) + n - 1)) return false;
   void* q = const_cast<void*>(p);
   if (hipHostRegister(q, n, ro ? hipHostRegisterReadOnly : hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();  // (e.g. a registration inside the range)
+    return false;
+  }
+  // A range that shares its first page with an older registration registers,
+  // but HIP then resolves its first byte to the older one, and an async DMA of
+  // the whole range fails: only a range that now resolves as one buffer from
+  // end to end counts (the staging copy takes the rest).
+  if (!host_pinned(p, n)) {
+    (void)hipHostUnregister(q);
     (void)hipGetLastError();
     return false;
   }

@@ -34,6 +34,7 @@ static void encode_fixed32(char* p, uint32_t v) {
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);  // (a crash keeps what was printed)
   std::mt19937_64 rng(20261015);
   const size_t n = 3000;
   std::vector<uint64_t> sizes(n);
@@ -133,6 +134,7 @@ int main() {
   EXPECT(nbad == 1 && oks[base9 + 4] == 0);
   if (reg) (void)hipHostUnregister(&files[7][0]);
 
+  fprintf(stderr, "section: small page-locked job\n");
   // ---- a small page-locked job (every image registered, <= 64 MiB): each
   // table one whole-image DMA and one kernel (or, LSBM_SMALL_LOCKED=zc, read
   // in place), tables spread over the stages: 6 tables, one empty, one with
@@ -208,6 +210,46 @@ int main() {
       close(fd);
       unlink(path);
     }
+  }
+
+  fprintf(stderr, "section: page locks next to the caller's registrations\n");
+  // ---- per-call page locks next to the caller's own registrations: an image
+  // that shares its first page with a range the caller registered, and one
+  // that is registered in part.  The seal cannot lock them for the call, so it
+  // stages them; trailers are still the reference's, and the caller's own
+  // registrations are left as they were (unregistering them succeeds) ----
+  {
+    std::vector<uint64_t> sz(900);
+    for (auto& x : sz) x = 3000 + rng() % 2000;
+    uint64_t fs = 0;
+    const std::vector<lsbm::BlockHandle> hh = lsbm::LayoutBlocks(sz, &fs);
+    std::vector<uint8_t> yy(sz.size());
+    for (auto& x : yy) x = rng() & 1;
+    std::vector<char> big(2 * fs + (128u << 10));  // (img1 at +70017, img2 one image + 8 KiB later)
+    for (auto& c : big) c = (char)(' ' + rng() % 95);
+    char* base = big.data();
+    char* mid = base + 70001;  // the caller's range ends inside a page ...
+    char* img1 = mid + 16;     // ... that this image starts in
+    EXPECT(hipHostRegister(base, (size_t)(mid - base), hipHostRegisterDefault) == hipSuccess);
+    char* img2 = img1 + fs + 8192;  // registered in its first half by the caller
+    EXPECT(hipHostRegister(img2, fs / 2, hipHostRegisterDefault) == hipSuccess);
+    for (char* img : {img1, img2}) {
+      fprintf(stderr, "seal %s\n", img == img1 ? "img1" : "img2");
+      st = lsbm::SealBlocks(0, img, fs, hh.data(), yy.data(), hh.size());
+      if (!st.ok()) printf("status: %s\n", st.ToString().c_str());
+      EXPECT(st.ok());
+      for (size_t i = 0; i < hh.size(); i++) {
+        char trailer[5];
+        trailer[0] = (char)yy[i];
+        uint32_t crc = leveldb::crc32c::Extend(leveldb::crc32c::Value(img + hh[i].offset, hh[i].size), trailer, 1);
+        encode_fixed32(trailer + 1, leveldb::crc32c::Mask(crc));
+        EXPECT(memcmp(trailer, img + hh[i].offset + hh[i].size, 5) == 0);
+      }
+    }
+    fprintf(stderr, "unregister\n");
+    EXPECT(hipHostUnregister(img2) == hipSuccess);
+    EXPECT(hipHostUnregister(base) == hipSuccess);
+    fprintf(stderr, "section done\n");
   }
 
   // ---- error paths: a pipeline that fails with chunks in flight ----
