@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -32,8 +33,11 @@ namespace {
 // (common/log_writer.cc:33-40), so none crosses a window.  seal: res[4i..] =
 // the masked crc of record i (lsbm_log_crcs_dev, the image on the device is
 // not written); verify: res[i] = its checksum verdict (lsbm_log_verify_dev).
+// seal_into (seal only, nullable): instead of res, each chunk's masked crcs
+// are stored into the headers at seal_into + heads[i] (EncodeFixed32) as
+// soon as the chunk completes, under the later chunks' DMAs.
 Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint64_t* heads,
-               size_t n, bool seal, uint8_t* res) {
+               size_t n, bool seal, uint8_t* res, char* seal_into = nullptr) {
   if (n == 0) return Status::OK();
   HostTiming tm(seal ? "log_seal_device" : "log_verify_device");
   struct Chunk {
@@ -66,7 +70,16 @@ Status run_log(int device, const char* img, uint64_t lo, uint64_t hi, const uint
     if (tm.on) tm.add(HostTiming::kWait, HostTiming::now() - t), t = HostTiming::now();
     if (e != hipSuccess) return hip_status(e, seal ? "seal" : "verify");
     const Chunk& c = chunks[sg.tag];
-    memcpy(res + c.first * per, sg.res.h, c.count * per);
+    if (seal && seal_into) {
+      for (size_t i = 0; i < c.count; i++) {  // [masked crc LE32] at each header (log_writer.cc:85-88)
+        uint32_t m;
+        memcpy(&m, sg.res.h + 4 * i, 4);
+        char* h = seal_into + heads[c.first + i];
+        for (int b = 0; b < 4; b++) h[b] = (char)(m >> (8 * b));
+      }
+    } else {
+      memcpy(res + c.first * per, sg.res.h, c.count * per);
+    }
     if (tm.on) tm.add(HostTiming::kPost, HostTiming::now() - t);
     return Status::OK();
   };
@@ -452,7 +465,17 @@ Status BatchWriter::Seal(int device) {
   if (count == 0) return Status::OK();
   HostTiming tm("BatchWriter::Seal");
   // the unsealed tail of the log: every pending header's masked crc (4 B each
-  // come back), EncodeFixed32 into its header (util/coding.cc)
+  // come back), EncodeFixed32 into its header (util/coding.cc), chunk by
+  // chunk as the chunks complete.  LSBM_LOG_POST_AFTER=1 (A/B): all of them
+  // after the last chunk, over the worker pool.
+  static const bool post_after = getenv("LSBM_LOG_POST_AFTER") != nullptr;
+  if (!post_after) {
+    Status s = run_log(device, dest_.data(), headers_[sealed_], dest_.size(), &headers_[sealed_], count, true,
+                       nullptr, &dest_[0]);
+    if (!s.ok()) return s;
+    sealed_ = headers_.size();
+    return Status::OK();
+  }
   std::unique_ptr<uint32_t[]> masked(new uint32_t[count]);
   Status s = run_log(device, dest_.data(), headers_[sealed_], dest_.size(), &headers_[sealed_],
                      count, true, reinterpret_cast<uint8_t*>(masked.get()));
