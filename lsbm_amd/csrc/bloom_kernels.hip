@@ -800,6 +800,38 @@ constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 3
 #ifndef LSBM_PROBE_BLOCK_WAVES_PER_EU  // (A/B builds override)
 #define LSBM_PROBE_BLOCK_WAVES_PER_EU 1
 #endif
+#ifndef LSBM_BLOCK_AHEAD  // (A/B builds: 0 = each round's filter-block lookup after its own hash)
+#define LSBM_BLOCK_AHEAD 1
+#endif
+
+// FilterBlockReader::KeyMayMatch's filter lookup (table/filter_block.cc:78-109)
+// without the key: which filter of block [c, c + size) a data block at offset
+// doff uses.  kProbe: probe [f, f + len); kMay: "errors are treated as
+// potential matches"; kNo: an empty filter matches nothing.  base_lg is a
+// size_t loaded from a char, the shift count taken mod 64 (x86-64).
+enum : uint32_t { kBlkProbe = 0, kBlkMay = 1, kBlkNo = 2 };
+struct BlockTrailer {  // the block's last 5 bytes: the offset array's position and base_lg
+  uint32_t lg, lw;
+};
+__device__ __forceinline__ BlockTrailer block_trailer(uint64_t c, uint64_t size, uint64_t dummy) {
+  const bool ok = size >= 5;
+  BlockTrailer t;
+  t.lg = *reinterpret_cast<gcu8>(ok ? c + size - 1 : dummy);
+  t.lw = (uint32_t)load_le32(ok ? c + size - 5 : dummy);
+  return t;
+}
+// the offset array entry's address (or dummy, with *state = kBlkMay: no entry)
+__device__ __forceinline__ uint64_t block_entry(uint64_t c, uint64_t size, uint64_t doff, BlockTrailer t,
+                                                uint64_t dummy, uint32_t* state) {
+  const uint64_t base_lg = (uint64_t)(int64_t)(int8_t)(uint8_t)t.lg;
+  const uint64_t last_word = t.lw;
+  bool ok = size >= 5 && last_word <= size - 5;
+  const uint64_t num = ok ? (size - 5 - last_word) / 4 : 0;
+  const uint64_t index = doff >> (base_lg & 63u);
+  ok = ok && index < num;
+  *state = ok ? kBlkProbe : kBlkMay;
+  return ok ? c + last_word + index * 4 : dummy;
+}
 template <uint32_t kMode>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(kMode == kProbeFilter ? LSBM_PROBE_WAVES_PER_EU : LSBM_PROBE_BLOCK_WAVES_PER_EU)))
@@ -830,6 +862,34 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     plan = plan_span(kbase + oa0, n, avail, safe);
     fetch_span(plan, ch0, ch1);
   }
+  // Filter blocks, LSBM_BLOCK_AHEAD: a round's filter lookup does not depend
+  // on its keys, so it runs ahead of them as a pipeline -- the handle two
+  // rounds ahead, the block's trailer one round ahead before the hash, the
+  // offset-array entry one round ahead after it -- and a round's probes wait
+  // only for its hash (round 3: handle, trailer and entry one after another
+  // behind the hash).
+  constexpr bool kAhead = kMode == kProbeFilterBlock && LSBM_BLOCK_AHEAD;
+  const uint64_t fbase = reinterpret_cast<uint64_t>(a.base);
+  const uint64_t dummy = reinterpret_cast<uint64_t>(a.handles);  // (16 readable bytes)
+  uint64_t hc1 = 0, hs1 = 0, hd1 = 0;  // round r + 1's handle and data offset
+  uint64_t bf = 0;                     // round r's filter [bf, bf + blen), or its verdict bst
+  uint32_t blen = 0, bst = kBlkMay;
+  if constexpr (kAhead) {
+    const uint64_t q0q = q00 + lane < a.n ? q00 + lane : 0;
+    const uint64_t c0 = fbase + a.handles[2 * q0q], s0 = a.handles[2 * q0q + 1], d0 = a.data_offsets[q0q];
+    const BlockTrailer t0 = block_trailer(c0, s0, dummy);
+    const uint64_t e0 = block_entry(c0, s0, d0, t0, dummy, &bst);
+    const uint32_t st0 = (uint32_t)load_le32(e0), li0 = (uint32_t)load_le32(e0 + 4);
+    if (bst == kBlkProbe) {
+      bst = st0 <= li0 && li0 <= t0.lw ? kBlkProbe : st0 == li0 ? kBlkNo : kBlkMay;
+      bf = c0 + st0;
+      blen = li0 - st0;
+    }
+    const uint64_t q1q = q00 + stride + lane < a.n ? q00 + stride + lane : 0;
+    hc1 = fbase + a.handles[2 * q1q];
+    hs1 = a.handles[2 * q1q + 1];
+    hd1 = a.data_offsets[q1q];
+  }
   for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
@@ -837,10 +897,21 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     const uint64_t kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
     // the filter handle (and data offset) do not depend on the hash: requested
     // before it (the hash's LDS fences would otherwise hold them back)
-    const uint64_t qq = act ? q : 0;
-    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
-    const uint64_t size = a.handles[2 * qq + 1];
-    const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
+    uint64_t c = 0, size = 0, doff = 0;
+    uint64_t hc2 = 0, hs2 = 0, hd2 = 0;
+    BlockTrailer t1 = {0, 0};
+    if constexpr (kAhead) {
+      const uint64_t q2 = q + 2 * stride < a.n ? q + 2 * stride : 0;  // round r + 2's handle
+      hc2 = fbase + a.handles[2 * q2];
+      hs2 = a.handles[2 * q2 + 1];
+      hd2 = a.data_offsets[q2];
+      t1 = block_trailer(hc1, hs1, dummy);  // round r + 1's trailer
+    } else {
+      const uint64_t qq = act ? q : 0;
+      c = fbase + a.handles[2 * qq];
+      size = a.handles[2 * qq + 1];
+      doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
+    }
     // this round's chunks go to LDS; the next round's plan and loads go out
     const SpanPlan cur = plan;
     const u32x4 cc0 = ch0, cc1 = ch1;
@@ -854,17 +925,38 @@ void bloom_probe_kernel(BloomProbeArgs a) {
       if (q + 2 * stride < a.n) load_off2(a.key_offsets, q + 2 * stride, ob0, ob1);
     }
     const uint32_t h = staged_hash(stg, cur, cc0, cc1, ks, kn, act);
+    if constexpr (kAhead) {
+      // round r + 1's offset-array entry, then round r's probes
+      uint32_t st1;
+      const uint64_t e1 = block_entry(hc1, hs1, hd1, t1, dummy, &st1);
+      const uint32_t start1 = (uint32_t)load_le32(e1), limit1 = (uint32_t)load_le32(e1 + 4);
+      if (act) {
+        const bool may = bst == kBlkProbe ? key_may_match(bf, blen, h, a.k_use) : bst == kBlkMay;
+        a.may[q] = may ? 1 : 0;
+        hits += may ? 1u : 0u;
+      }
+      if (st1 == kBlkProbe)
+        st1 = start1 <= limit1 && limit1 <= t1.lw ? kBlkProbe : start1 == limit1 ? kBlkNo : kBlkMay;
+      bst = st1;
+      bf = hc1 + start1;
+      blen = limit1 - start1;
+      hc1 = hc2;
+      hs1 = hs2;
+      hd1 = hd2;
+      continue;
+    }
     if (!act) continue;
 #else
+    uint64_t c, size, doff;
   for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
     uint64_t ks = reinterpret_cast<uint64_t>(a.keys), kn = 0;
     if (act) key_extent(a.keys, a.key_offsets, q, a.strip, ks, kn);
     const uint64_t qq = act ? q : 0;
-    const uint64_t c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
-    const uint64_t size = a.handles[2 * qq + 1];
-    const uint64_t doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
+    c = reinterpret_cast<uint64_t>(a.base) + a.handles[2 * qq];
+    size = a.handles[2 * qq + 1];
+    doff = a.mode == kProbeFilter ? 0 : a.data_offsets[qq];
     const uint32_t h = wave_hash(stg, kProbeStageWords * 4u - 48u, ks, kn, act);
     if (!act) continue;
 #endif
