@@ -179,9 +179,11 @@ __device__ __forceinline__ uint32_t hash_key_lds_uniform(const uint32_t* stg, ui
   }
   if (r) {
     const uint32_t x = __builtin_amdgcn_alignbyte(w[t + 1], lo, sh);
-    if (r == 3) h += sext8(x >> 16) << 16;
-    if (r >= 2) h += sext8(x >> 8) << 8;
-    h += sext8(x);
+    // the r tail bytes, each sign-extended, at once: sext8(b) << 8i =
+    // (b << 8i) - ((b & 0x80) << (8i + 1)), with wave-uniform masks
+    // (5 VALU against 12 for the three-step form)
+    const uint32_t m = 0xffffffffu >> (32u - 8u * r), m80 = 0x80808080u & m;
+    h += (x & m) - ((x & m80) << 1);
     h *= kHashM;
     h ^= h >> 24;
   }
@@ -372,20 +374,40 @@ __device__ __forceinline__ void load_off2(const uint64_t* ko, uint64_t i, uint64
 struct SpanPlan {
   uint64_t sbase;  // 16-B aligned start (staged), or a safe 16-B aligned address
   uint32_t nch;    // chunks, 0 when not staged
+  uint32_t n0;     // the first non-empty key's length (staged_hash's one-length test)
 };
 
+// Wave masks of one compare each, straight from the v_cmp (a __ballot of a
+// compound condition compiles to a select and a second compare per lane:
+// 2 VALU more per ballot).  Inactive lanes read as 0.
+enum : int { kCmpNe = 33, kCmpUgt = 34, kCmpUlt = 36 };
+__device__ __forceinline__ uint64_t lanes_ne64(uint64_t a, uint64_t b) { return __builtin_amdgcn_uicmpl(a, b, kCmpNe); }
+__device__ __forceinline__ uint64_t lanes_ult64(uint64_t a, uint64_t b) { return __builtin_amdgcn_uicmpl(a, b, kCmpUlt); }
+__device__ __forceinline__ uint64_t lanes_ugt64(uint64_t a, uint64_t b) { return __builtin_amdgcn_uicmpl(a, b, kCmpUgt); }
+__device__ __forceinline__ uint64_t lanes_ne(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, kCmpNe); }
+__device__ __forceinline__ uint64_t lanes_ult(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, kCmpUlt); }
+// lanes [0, m) of the wave (m wave-uniform): scalar only
+__device__ __forceinline__ uint64_t first_lanes(uint64_t m) { return m >= 64 ? ~0ull : (1ull << m) - 1ull; }
+
 __device__ __forceinline__ SpanPlan plan_span(uint64_t s, uint64_t n, uint32_t cap, uint64_t safe) {
-  const uint64_t nz = __ballot(n > 0);
+  const uint64_t nz = lanes_ne64(n, 0);
   const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
   const uint32_t ll = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
   const uint64_t lo = readlane64(s, fl), hi = readlane64(s + n, ll);
   const uint64_t sbase = lo & ~15ull;
-  const bool inside = n == 0 || (s >= lo && s + n <= hi);
-  const bool staged = nz != 0 && hi > lo && hi - sbase <= cap && hi - sbase <= 2048u &&
-                      __ballot(!inside) == 0ull;
+  // a non-empty key outside [lo, hi)
+  const uint64_t outside = nz & (lanes_ult64(s, lo) | lanes_ugt64(s + n, hi));
+  // lo < hi <= lo + 2048 iff hi - lo - 1 < 2048 (64-bit), and then the span
+  // [sbase, hi) fits 32 bits: scalar compares only (a 64-bit compare of two
+  // wave-uniform values goes to the VALU)
+  const uint64_t d1 = hi - lo - 1u;
+  const uint32_t span = (uint32_t)d1 + 1u + ((uint32_t)lo & 15u);
+  const bool staged = nz != 0 && (uint32_t)(d1 >> 32) == 0u && (uint32_t)d1 < 2048u && span <= 2048u && span <= cap &&
+                      outside == 0ull;
   SpanPlan p;
   p.sbase = staged ? sbase : safe;
-  p.nch = staged ? (uint32_t)((hi - sbase + 15) >> 4) : 0u;
+  p.nch = staged ? (span + 15u) >> 4 : 0u;
+  p.n0 = (uint32_t)readlane64(n, fl);
   return p;
 }
 
@@ -399,20 +421,19 @@ __device__ __forceinline__ void fetch_span(const SpanPlan& p, u32x4& c0, u32x4& 
   c1 = *reinterpret_cast<gcu32x4>(a1);
 }
 
+// (actm: the wave's active lanes, act = bit lane of actm)
 __device__ __forceinline__ uint32_t staged_hash(uint32_t* stg, const SpanPlan& p, u32x4 c0, u32x4 c1,
-                                                uint64_t s, uint64_t n, bool act) {
+                                                uint64_t s, uint64_t n, bool act, uint64_t actm) {
   const uint32_t lane = threadIdx.x & 63u;
   if (p.nch == 0) return hash_key_batched(s, n, kBloomSeed);
   if (lane < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * lane) = c0;
   if (lane + 64u < p.nch) *reinterpret_cast<u32x4*>(stg + 4 * (lane + 64u)) = c1;
   wave_phase();
-  const uint64_t nz = __ballot(n > 0);
-  const uint32_t fl = nz ? (uint32_t)__builtin_ctzll(nz) : 0u;
   const uint32_t rel = act ? (uint32_t)(s - p.sbase) : 0u;
-  const uint32_t n0 = (uint32_t)readlane64(n, fl);
   uint32_t h;
-  if (__ballot(act && n != n0) == 0ull)
-    h = hash_key_lds_uniform(stg, rel, __builtin_amdgcn_readfirstlane(n0), kBloomSeed);
+  // (staged: every key is inside the span, n < 2 KiB)
+  if ((lanes_ne((uint32_t)n, p.n0) & actm) == 0ull)
+    h = hash_key_lds_uniform(stg, rel, p.n0, kBloomSeed);
   else
     h = hash_key_lds(stg, rel, (uint32_t)n, kBloomSeed);
   wave_phase();  // (the next round's staging writes after these reads)
@@ -466,9 +487,6 @@ __device__ void build_one(const BloomBuildArgs& a, uint64_t k0, uint64_t k1, uin
 // leaves LDS once.  The round's key words are staged in the region's free
 // tail (wave_hash).  Otherwise the group's filters go one by one through
 // build_one.
-#ifndef LSBM_BUILD_DEPTH  // (A/B builds override)
-#define LSBM_BUILD_DEPTH 1
-#endif
 // LDS byte address of p (a pointer into __shared__ memory), and the LDS word
 // holding bit b (an LDS bit address) or-ed with v
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -596,78 +614,58 @@ void bloom_build_kernel(BloomBuildArgs a) {
     const uint32_t used = (uint32_t)((total + 3u) & ~3ull) * 4u;
     uint32_t* stg = bm + used / 4u;
     const uint32_t avail = used + 48u < kBloomRegionWords * 4u ? kBloomRegionWords * 4u - used - 48u : 0u;
+    // A round's key (start, length) is computed once, with its span plan a
+    // round ahead, and carried to the round.
+    // A round's key (start, length) is computed once, with its span plan a
+    // round ahead, and carried to the round.  (Tried: two register sets
+    // alternating between rounds, which drops the 6 v_mov_b64 a round that
+    // move the next round's set into the current one: no faster, twice the
+    // code; profiles/r04/check26/.)
     SpanPlan plan;
     u32x4 ch0, ch1;
+    uint64_t ks = 0, kn = 0;
     {
       const bool act = lane < nkeys;
-      const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
-      plan = plan_span(kbase + oa0, n, avail, safe);
+      kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+      ks = kbase + oa0;
+      plan = plan_span(ks, kn, avail, safe);
       fetch_span(plan, ch0, ch1);
     }
-#if LSBM_BUILD_DEPTH == 2
-    // (A/B: key words two rounds ahead, offsets three)
-    uint64_t oc0 = 0, oc1 = 0;
-    if (lane + 128u < nkeys) load_off2(ko, lane + 128, oc0, oc1);
-    SpanPlan plan2;
-    u32x4 ch2, ch3;
-    {
-      const bool act1 = lane + 64u < nkeys;
-      const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-      plan2 = plan_span(kbase + ob0, n1, avail, safe);
-      fetch_span(plan2, ch2, ch3);
-    }
-#endif
+    uint32_t c0 = 0;  // filters starting before the round
     for (uint32_t r0 = 0; r0 < nkeys; r0 += 64) {  // wave-uniform rounds
       const uint32_t r = r0 + lane;
+      const uint64_t actm = first_lanes(nkeys - r0);
       const bool act = r < nkeys;
       // the last filter of the group whose first key is <= r (empty filters
       // share their successor's first key and are passed over): the filters
-      // starting before the round (a ballot), plus those starting inside it at
-      // or before r -- a wave-uniform handful (~2 of 33-key filters per
-      // 64-key round), each read with readlane.  (Round 3: a 5-step binary
-      // search, a chain of dependent ds_bpermute round trips every round.)
-      const uint32_t c0 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0));
-      const uint32_t c1 = (uint32_t)__builtin_popcountll(__ballot(lane < kBloomGroup && st_t < r0 + 64u));
+      // starting before the round, plus those starting inside it at or before
+      // r -- a wave-uniform handful (~2 of 33-key filters per 64-key round),
+      // each read with readlane.  (Round 3: a 5-step binary search, a chain
+      // of dependent ds_bpermute round trips every round.)  st_t is ~0 past
+      // the group: one compare counts the group's filters.
+      const uint32_t c1 = (uint32_t)__builtin_popcountll(lanes_ult(st_t, r0 + 64u));
       uint32_t cnt = c0;
       for (uint32_t q = c0; q < c1; q++)
         cnt += (uint32_t)__builtin_amdgcn_readlane((int)st_t, (int)q) <= r ? 1u : 0u;
+      c0 = c1;
       const uint32_t j = cnt - 1u;  // (filter 0 starts at key 0: cnt >= 1)
       const uint4 sl = slots[wv][j];
       const uint32_t bbase = sl.x, d = sl.y;
       const uint64_t M = ((uint64_t)sl.w << 32) | sl.z;
       const uint32_t c32 = slot_c32[wv][j];
-      const uint64_t s = kbase + oa0;
-      const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+      const uint64_t s = ks, n = kn;
       // this round's chunks into LDS, then the next round's plan and loads
       const SpanPlan cur = plan;
       const u32x4 cc0 = ch0, cc1 = ch1;
-#if LSBM_BUILD_DEPTH == 2
-      plan = plan2;
-      ch0 = ch2;
-      ch1 = ch3;
-      {
-        const bool act2 = r + 128u < nkeys;
-        const uint64_t n2 = act2 && oc1 >= oc0 + a.strip ? oc1 - oc0 - a.strip : 0;
-        plan2 = plan_span(kbase + oc0, n2, avail, safe);
-        fetch_span(plan2, ch2, ch3);
-        oa0 = ob0;
-        oa1 = ob1;
-        ob0 = oc0;
-        ob1 = oc1;
-        if (r + 192u < nkeys) load_off2(ko, r + 192, oc0, oc1);
-      }
-#else
       {
         const bool act1 = r + 64u < nkeys;
-        const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-        plan = plan_span(kbase + ob0, n1, avail, safe);
+        kn = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
+        ks = kbase + ob0;
+        plan = plan_span(ks, kn, avail, safe);
         fetch_span(plan, ch0, ch1);
-        oa0 = ob0;
-        oa1 = ob1;
         if (r + 128u < nkeys) load_off2(ko, r + 128, ob0, ob1);
       }
-#endif
-      const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act);
+      const uint32_t h = staged_hash(stg, cur, cc0, cc1, s, n, act, actm);
       if (!act) continue;
       const uint32_t delta = (h >> 17) | (h << 15);  // util/bloom.cc:56-61
       ProbeSeq ps = probe_seq(h, delta, fastmod(h, M, d), fastmod(delta, M, d), c32, d);
@@ -798,7 +796,7 @@ constexpr uint32_t kProbeStageWords = 576;  // a wave's key staging area (64 x 3
 #define LSBM_PROBE_WAVES_PER_EU 6
 #endif
 #ifndef LSBM_PROBE_BLOCK_WAVES_PER_EU  // (A/B builds override)
-#define LSBM_PROBE_BLOCK_WAVES_PER_EU 1
+#define LSBM_PROBE_BLOCK_WAVES_PER_EU 5  // (<= 96 VGPRs: the pipelined lookups fit without spills)
 #endif
 #ifndef LSBM_BLOCK_AHEAD  // (A/B builds: 0 = each round's filter-block lookup after its own hash)
 #define LSBM_BLOCK_AHEAD 1
@@ -854,12 +852,15 @@ void bloom_probe_kernel(BloomProbeArgs a) {
   uint64_t oa0 = 0, oa1 = 0, ob0 = 0, ob1 = 0;
   if (q00 + lane < a.n) load_off2(a.key_offsets, q00 + lane, oa0, oa1);
   if (q00 + stride + lane < a.n) load_off2(a.key_offsets, q00 + stride + lane, ob0, ob1);
+  // (a round's key start and length: computed once, with its plan, and carried)
   SpanPlan plan;
   u32x4 ch0, ch1;
+  uint64_t ksn = 0, knn = 0;
   {
     const bool act = q00 + lane < a.n;
-    const uint64_t n = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;
-    plan = plan_span(kbase + oa0, n, avail, safe);
+    knn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+    ksn = kbase + oa0;
+    plan = plan_span(ksn, knn, avail, safe);
     fetch_span(plan, ch0, ch1);
   }
   // Filter blocks, LSBM_BLOCK_AHEAD: a round's filter lookup does not depend
@@ -893,8 +894,8 @@ void bloom_probe_kernel(BloomProbeArgs a) {
   for (uint64_t q0 = q00; q0 < a.n; q0 += stride) {
     const uint64_t q = q0 + lane;
     const bool act = q < a.n;
-    const uint64_t ks = kbase + oa0;
-    const uint64_t kn = act && oa1 >= oa0 + a.strip ? oa1 - oa0 - a.strip : 0;  // key_extent
+    const uint64_t actm = first_lanes(a.n - q0);
+    const uint64_t ks = ksn, kn = knn;
     // the filter handle (and data offset) do not depend on the hash: requested
     // before it (the hash's LDS fences would otherwise hold them back)
     uint64_t c = 0, size = 0, doff = 0;
@@ -917,14 +918,13 @@ void bloom_probe_kernel(BloomProbeArgs a) {
     const u32x4 cc0 = ch0, cc1 = ch1;
     {
       const bool act1 = q + stride < a.n;
-      const uint64_t n1 = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
-      plan = plan_span(kbase + ob0, n1, avail, safe);
+      knn = act1 && ob1 >= ob0 + a.strip ? ob1 - ob0 - a.strip : 0;
+      ksn = kbase + ob0;
+      plan = plan_span(ksn, knn, avail, safe);
       fetch_span(plan, ch0, ch1);
-      oa0 = ob0;
-      oa1 = ob1;
       if (q + 2 * stride < a.n) load_off2(a.key_offsets, q + 2 * stride, ob0, ob1);
     }
-    const uint32_t h = staged_hash(stg, cur, cc0, cc1, ks, kn, act);
+    const uint32_t h = staged_hash(stg, cur, cc0, cc1, ks, kn, act, actm);
     if constexpr (kAhead) {
       // round r + 1's offset-array entry, then round r's probes
       uint32_t st1;
