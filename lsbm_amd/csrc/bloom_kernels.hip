@@ -742,6 +742,9 @@ __device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_u
   // chunk (min(k_use, 16) probes) is requested together with the k byte:
   // one round trip less per lookup (those past k are loaded and ignored).
   const uint32_t k0n = k_use < 16 ? (uint32_t)k_use : 16u;
+#ifdef LSBM_DIAG_NO_FILTER_LOADS  // (diagnostic A/B builds only: what the filter round trip costs)
+  return ((ps.pos ^ ps.dm ^ (uint32_t)f) & 1u) != 0;
+#endif
   const uint8_t kb = *reinterpret_cast<gcu8>(f + len - 1);
   uint32_t v[16], bit[16];
 #pragma unroll

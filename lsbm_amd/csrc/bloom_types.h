@@ -9,7 +9,7 @@
 // is only ever written under build/ab/ (tools/build_variant.sh), never the
 // product lsbm_amd/liblsbm_crc32c.so.
 #if (defined(LSBM_DIAG_NO_STORE) || defined(LSBM_DIAG_VERIFY_WRITEBACK) || \
-     defined(LSBM_DIAG_NO_PROBE_WRITES)) && !defined(LSBM_DIAG_BUILD)
+     defined(LSBM_DIAG_NO_PROBE_WRITES) || defined(LSBM_DIAG_NO_FILTER_LOADS)) && !defined(LSBM_DIAG_BUILD)
 #error "LSBM_DIAG_* result-changing macros need LSBM_DIAG_BUILD (A/B variant builds only)"
 #endif
 

@@ -31,7 +31,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM = 8000.0  # GB/s, MI355X spec
-KLEN, PER, BPK = 31, 33, 20
+KLEN, PER, BPK = 31, 33, int(os.environ.get("LSBM_BENCH_BPK", "20"))  # (env: diagnostic k sweeps)
 
 
 def dbbench_keys_dev(torch, n, first=0, seq0=1):
