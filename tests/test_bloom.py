@@ -382,6 +382,33 @@ def test_gpu_may_match_reference_vectors(torch_cuda, bloom_golden, bloom_oracle)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [(1 << 28) + 2, (1 << 29) + 2], ids=["2^31+8_bits", "2^32+8_bits"])
+def test_gpu_may_match_filters_past_2_31_bits(torch_cuda, bloom_oracle, nbytes):
+    """Filters of >= 2^31 bits take a remainder per probe (util/bloom.cc:84:
+    the lookup's incremental probe step needs bits < 2^31), and past 2^32
+    bits h % bits is h itself: both wide paths against the reference's loop.
+    Synthetic filter bytes with ~7/8 of the bits set, so that both answers
+    occur; the stored k byte is 6."""
+    from lsbm_amd import bloom
+    torch = torch_cuda
+    rng = np.random.default_rng(nbytes)
+    f = np.frombuffer(rng.bytes(nbytes), np.uint8).copy()
+    f |= np.frombuffer(rng.bytes(nbytes), np.uint8)
+    f |= np.frombuffer(rng.bytes(nbytes), np.uint8)
+    f[-1] = 6
+    keys = random_keys(nbytes & 0xffff, 3000, 1, 30)
+    nq = keys[1].size - 1
+    handles = np.tile(np.array([0, nbytes], dtype=np.int64), nq)
+    may, n_may = bloom.may_match(_dev(torch, f), _dev(torch, handles), _dev(torch, keys[0]),
+                                 _dev(torch, _i64(keys[1])), 10, 15)
+    got = may.cpu().numpy()
+    want = np.array([bloom_oracle.key_may_match(key_at(keys, i), f, 10, 15) for i in range(nq)],
+                    dtype=np.uint8)
+    assert np.array_equal(got, want)
+    assert 0 < int(want.sum()) < nq and int(n_may.item()) == int(want.sum())
+
+
+@pytest.mark.gpu
 def test_gpu_filter_block_lookups_reference_vectors(torch_cuda, bloom_golden, bloom_oracle):
     """FilterBlockReader::KeyMayMatch on every fixture block, as built and
     corrupted, in one launch per scenario."""
