@@ -255,11 +255,10 @@ struct ProbeSeq {
     pos = min(p, p - d);
   }
 };
-// The lookup side's form (key_may_match, an out-of-line call per query): the
-// carry's correction applied after the step, which needs no second step
-// register -- the probe kernel's caller then keeps its live registers across
-// the call (with the selected-step form it spilled 16 B per lane per query:
-// 0.49 -> 0.55 ms, profiles/r04/check5/bench_bloom.log).
+// The lookup side's form (key_may_match): the carry's correction applied
+// after the step, which needs no second step register (with the
+// selected-step form the lookup, then an out-of-line call, spilled 16 B per
+// lane per query: 0.49 -> 0.55 ms, profiles/r04/check5/bench_bloom.log).
 struct ProbeSeqLookup {
   uint32_t pos, dm, c32, d, h, delta;
   __device__ __forceinline__ void next() {
@@ -721,8 +720,12 @@ __device__ __forceinline__ uint64_t load_le32(uint64_t p) {  // DecodeFixed32, a
   return (uint64_t)b[0] | ((uint64_t)b[1] << 8) | ((uint64_t)b[2] << 16) | ((uint64_t)b[3] << 24);
 }
 
-// util/bloom.cc:65-89 on the filter [f, f + len).
-__device__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_use) {
+// util/bloom.cc:65-89 on the filter [f, f + len).  Inlined: as a call, its
+// entry waited for every load the probe kernel had in flight (the next
+// rounds' key words and offsets); inlined the kernels still fit 80 / 95 VGPRs
+// (6 / 5 waves per SIMD): 0.449 -> 0.441 ms one filter per query, 0.535 ->
+// 0.511 ms through filter blocks (profiles/r04/check30/).
+__device__ __forceinline__ bool key_may_match(uint64_t f, uint64_t len, uint32_t h, uint64_t k_use) {
   if (len < 2) return false;
   const uint64_t bits = (len - 1) * 8;
   const BitMod m = bit_mod(bits);
