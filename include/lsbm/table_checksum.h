@@ -47,8 +47,21 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
 
 // Batched ReadBlock verify.  ok (optional) receives one flag per block.
 // Returns Corruption("block checksum mismatch") if any block fails.
+//
+// The image's memory decides how it reaches the device:
+//  * `char*` -- writable memory the caller owns, as lsbm's ReadBlock has it:
+//    it preads every block into `new char[n + kBlockTrailerSize]`
+//    (table/format.cc:79-82; lsbm reads no table through mmap,
+//    util/env_posix.cc:329-330).  A small job's image is page-locked for the
+//    call and DMA-ed in place, as the seal's is (no staging copy);
+//  * `const char*` -- possibly a read-only mapping (an mmap'd table file),
+//    which must not be pinned for writing (that could copy a private
+//    mapping's pages out of the page cache): staged through pinned buffers
+//    unless the caller page-locked it.
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
                     size_t n, std::vector<uint8_t>* ok);
+Status VerifyBlocks(int device, char* file, size_t file_size, const BlockHandle* handles, size_t n,
+                    std::vector<uint8_t>* ok);
 
 // One table file image in host memory: its blocks and, for sealing, their
 // CompressionType bytes.
@@ -67,8 +80,14 @@ struct TableImage {
 // back from the device.  VerifyTables' ok holds the tables' flags one after
 // the other.  A page-locked image (hipHostMalloc / hipHostRegister) is DMA-ed
 // in place; a pageable one is copied into pinned staging first.
+// VerifyTables' images are read-only memory unless `memory` says they are
+// writable heap buffers (see VerifyBlocks); SealTables writes its images, so
+// they are writable by definition.
+enum ImageMemory : uint8_t { kImagesReadOnly = 0, kImagesWritable = 1 };
 Status SealTables(int device, const TableImage* tables, size_t count);
 Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok);
+Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok,
+                    ImageMemory memory);
 
 }  // namespace lsbm
 

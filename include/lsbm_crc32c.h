@@ -225,12 +225,27 @@ int lsbm_test_pci_numa_node(const char* sysfs_root, const char* bus_id);
 int lsbm_test_parse_cpulist(const char* list, int* cpus, int cap);
 int lsbm_test_cgroup_quota(const char* cgroup_root);
 int lsbm_test_pool_overlap(int callers, int jobs, int pieces, int piece_us, double* seconds);
+/* Testing: the quota of the process's own cgroup as usable_cores() finds it:
+ * `proc_cgroup` is the text of /proc/self/cgroup, resolved under the cgroup
+ * mount `cgroup_root` (the smallest quota over the cgroup and its ancestors;
+ * the mount root's when none). */
+int lsbm_test_cgroup_quota_of(const char* cgroup_root, const char* proc_cgroup);
+/* Testing: one job of `pieces` pieces that each sleep `piece_us`, with at
+ * most `max_helpers` pool workers joining the caller (-1: any number);
+ * returns how many distinct threads ran its pieces. */
+int lsbm_test_pool_helpers(int pieces, int piece_us, int max_helpers);
+/* Testing: page ranges currently page-locked by the C++ layers' per-call
+ * locks (0 whenever no call is running), and how many ranges they have
+ * page-locked since start-up (which calls DMA-ed an image in place). */
+int lsbm_test_locked_ranges(void);
+long lsbm_test_locks_taken(void);
 /* Testing: `callers` threads each run `jobs` parallel jobs of 1..max_pieces
  * pieces (some with nested jobs); returns how many pieces did not run exactly
  * once (0 = correct), -1 for bad arguments. */
 int lsbm_test_pool_stress(int callers, int jobs, int max_pieces);
 /* Testing: 1 if the C++ layers would DMA [p, p + n) in place (page-locked by
- * hipHostMalloc or one hipHostRegister covering the whole range), else 0. */
+ * hipHostMalloc or one hipHostRegister covering the whole range, and no page
+ * of it held by another call's per-call lock), else 0. */
 int lsbm_test_host_pinned(const void* p, size_t n);
 /* Testing: page-locked table jobs up to `mb` MiB take the small-job path
  * (each table one whole-image DMA and one kernel on a stage's stream, or with

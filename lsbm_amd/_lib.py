@@ -58,6 +58,10 @@ SIGNATURES = {
     "lsbm_test_pci_numa_node": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "lsbm_test_parse_cpulist": (_int, [ctypes.c_char_p, _vp, _int]),
     "lsbm_test_cgroup_quota": (_int, [ctypes.c_char_p]),
+    "lsbm_test_cgroup_quota_of": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "lsbm_test_pool_helpers": (_int, [_int, _int, _int]),
+    "lsbm_test_locked_ranges": (_int, []),
+    "lsbm_test_locks_taken": (ctypes.c_long, []),
     "lsbm_test_pool_overlap": (_int, [_int, _int, _int, _int, _vp]),
     "lsbm_test_host_pinned": (_int, [_vp, _sz]),
     "lsbm_test_host_copy": (_int, [_vp, _vp, _sz, _int]),

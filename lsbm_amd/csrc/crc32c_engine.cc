@@ -745,15 +745,19 @@ __attribute__((visibility("default"))) int lsbm_crc32c_batch_host(int device, co
         e = hipMemcpyAsync(d_data, src + h_offsets[next], bytes, hipMemcpyHostToDevice, s.stream);
     } else {
       // gather over the worker pool: runs of blocks of about equal bytes
-      const uint64_t ways = 2 * ((uint64_t)pool_threads() + 1);
+      const int helpers = copy_helpers();
+      const uint64_t ways = 2 * ((uint64_t)helpers + 1);
       const uint64_t per = std::max<uint64_t>(1, (cnt + ways - 1) / ways);
-      parallel_for(bytes < (512u << 10) ? 1 : (size_t)((cnt + per - 1) / per), [&](size_t r) {
-        const uint64_t k0 = next + r * per, k1 = std::min(last, k0 + per);
-        for (uint64_t k = k0; k < k1; k++) {
-          const uint64_t s0 = h_offsets[k], s1 = h_offsets[k + 1];
-          if (s1 > s0) memcpy(s.bulk.h + off[k - next], src + s0, s1 - s0);
-        }
-      });
+      parallel_for(
+          bytes < (512u << 10) ? 1 : (size_t)((cnt + per - 1) / per),
+          [&](size_t r) {
+            const uint64_t k0 = next + r * per, k1 = std::min(last, k0 + per);
+            for (uint64_t k = k0; k < k1; k++) {
+              const uint64_t s0 = h_offsets[k], s1 = h_offsets[k + 1];
+              if (s1 > s0) memcpy(s.bulk.h + off[k - next], src + s0, s1 - s0);
+            }
+          },
+          helpers);
       e = hipMemcpyAsync(s.bulk.d, s.bulk.h, meta_off + meta_n, hipMemcpyHostToDevice, s.stream);
     }
     if (e != hipSuccess) {

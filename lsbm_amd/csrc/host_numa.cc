@@ -127,6 +127,78 @@ int cgroup_cpu_quota(const char* cgroup_root) {
   return 0;
 }
 
+namespace {
+// Quota of one cgroup directory: v2 cpu.max, else v1 cfs files (0: none).
+int dir_quota(const std::string& dir, bool v2) {
+  std::string s;
+  if (v2) {
+    char q[32] = {0};
+    long long period = 0;
+    if (read_file(dir + "/cpu.max", &s) && sscanf(s.c_str(), "%31s %lld", q, &period) == 2 &&
+        strcmp(q, "max") != 0 && period > 0 && atoll(q) > 0)
+      return (int)std::max<long long>(1, atoll(q) / period);
+    return 0;
+  }
+  std::string ps;
+  if (read_file(dir + "/cpu.cfs_quota_us", &s) && read_file(dir + "/cpu.cfs_period_us", &ps)) {
+    const long long quota = atoll(s.c_str()), period = atoll(ps.c_str());
+    if (quota > 0 && period > 0) return (int)std::max<long long>(1, quota / period);
+  }
+  return 0;
+}
+
+// The smallest quota on the way from `path` (a cgroup path, "/a/b") up to the
+// hierarchy's root under `mount`: a parent's limit binds its children too.
+int path_quota(const std::string& mount, std::string path, bool v2) {
+  int best = 0;
+  for (;;) {
+    while (path.size() > 1 && path.back() == '/') path.pop_back();
+    const int q = dir_quota(path == "/" ? mount : mount + path, v2);
+    if (q > 0) best = best ? std::min(best, q) : q;
+    const size_t cut = path.rfind('/');
+    if (path.empty() || path == "/" || cut == std::string::npos) break;
+    path = cut == 0 ? "/" : path.substr(0, cut);
+  }
+  return best;
+}
+}  // namespace
+
+int cgroup_cpu_quota_of(const char* cgroup_root, const char* proc_cgroup) {
+  const std::string root(cgroup_root ? cgroup_root : "/sys/fs/cgroup");
+  std::string v2_path, v1_path;
+  bool have_v2 = false, have_v1 = false;
+  const char* p = proc_cgroup ? proc_cgroup : "";
+  while (*p) {  // lines "<id>:<controllers>:<path>"
+    const char* eol = strchr(p, '\n');
+    const std::string line(p, eol ? eol - p : strlen(p));
+    p = eol ? eol + 1 : p + line.size();
+    const size_t a = line.find(':'), b = a == std::string::npos ? a : line.find(':', a + 1);
+    if (b == std::string::npos) continue;
+    const std::string id = line.substr(0, a), ctl = line.substr(a + 1, b - a - 1), path = line.substr(b + 1);
+    if (id == "0" && ctl.empty()) {
+      have_v2 = true;
+      v2_path = path;
+      continue;
+    }
+    for (size_t s = 0; s <= ctl.size();) {  // v1: "cpu" among the controllers
+      size_t e = ctl.find(',', s);
+      if (e == std::string::npos) e = ctl.size();
+      if (ctl.compare(s, e - s, "cpu") == 0) {
+        have_v1 = true;
+        v1_path = path;
+      }
+      s = e + 1;
+    }
+  }
+  int q = 0;
+  if (have_v2) q = path_quota(root, v2_path, true);
+  if (!q && have_v1) {
+    q = path_quota(root + "/cpu", v1_path, false);
+    if (!q) q = path_quota(root + "/cpu,cpuacct", v1_path, false);
+  }
+  return q ? q : cgroup_cpu_quota(cgroup_root);  // (the mount root: a cgroup namespace's own)
+}
+
 int usable_cores() {
   static const int n = [] {
     if (const char* v = getenv("LSBM_HOST_THREADS")) {
@@ -135,7 +207,9 @@ int usable_cores() {
     }
     int c = (int)affinity_cpus().size();
     if (c <= 0) c = (int)std::max(1L, sysconf(_SC_NPROCESSORS_ONLN));
-    const int q = cgroup_cpu_quota(nullptr);
+    std::string self;
+    const int q = read_file("/proc/self/cgroup", &self) ? cgroup_cpu_quota_of(nullptr, self.c_str())
+                                                         : cgroup_cpu_quota(nullptr);
     return q > 0 ? std::min(c, q) : c;
   }();
   return n;
@@ -216,5 +290,9 @@ __attribute__((visibility("default"))) int lsbm_test_parse_cpulist(const char* l
 }
 __attribute__((visibility("default"))) int lsbm_test_cgroup_quota(const char* cgroup_root) {
   return lsbm::cgroup_cpu_quota(cgroup_root);
+}
+__attribute__((visibility("default"))) int lsbm_test_cgroup_quota_of(const char* cgroup_root,
+                                                                     const char* proc_cgroup) {
+  return lsbm::cgroup_cpu_quota_of(cgroup_root, proc_cgroup);
 }
 }  // extern "C"

@@ -40,6 +40,12 @@ bool node_cpulist(const char* sysfs_root, int node, std::vector<int>* cpus);
 // (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us; 0 if none).
 std::vector<int> affinity_cpus();
 int cgroup_cpu_quota(const char* cgroup_root);
+// The quota of the process's own cgroup: its path from `proc_cgroup` (the
+// text of /proc/self/cgroup: the v2 "0::<path>" line, else the v1 line whose
+// controllers include cpu) under the mount `cgroup_root`, the smallest over
+// that directory and its ancestors; the mount root's own quota when none is
+// found there (a cgroup namespace shows its cgroup as "/").
+int cgroup_cpu_quota_of(const char* cgroup_root, const char* proc_cgroup);
 
 // Threads worth running at once: the affinity mask's CPUs, capped by the
 // cgroup quota (the GPU box: 256 CPUs in the mask, a quota of 16).

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,7 +41,7 @@ bool pinned_byte(const void* p) {
 // [p, p + n) page-locked: its first and last bytes are, and the allocation
 // holding p (when the runtime reports one) spans the whole range, so that a
 // registered prefix of a larger buffer does not pass as pinned.
-bool host_pinned(const void* p, size_t n) {
+static bool pinned_range(const void* p, size_t n) {
   if (!p || n == 0 || !pinned_byte(p)) return false;
   const char* last = static_cast<const char*>(p) + (n - 1);
   if (!pinned_byte(last)) return false;
@@ -63,16 +64,70 @@ bool host_pinned(const void* p, size_t n) {
   return false;
 }
 
+// ---- the library's own per-call page locks ----
+// Every hipHostRegister / hipHostUnregister the library makes for a call
+// (CallLocks), and every "is this range page-locked?" question the layers
+// ask, happen under one process-wide mutex, against the set of page ranges
+// that live CallLocks hold.  Round 4 checked "both ends unregistered" and
+// then registered as two steps: two concurrent calls whose images share a
+// page could both pass the check, and the loser's unregister could break the
+// winner's registration with its DMA in flight.  Now:
+//   * a range that touches a page a live CallLocks holds is never registered
+//     again (it takes the staging copy);
+//   * a range on such a page never counts as page-locked either: its bytes
+//     may lie inside another call's registration, which that call drops when
+//     it returns, so an in-place DMA from them could outlive it.
+namespace {
+std::mutex g_lock_mu;
+std::map<uintptr_t, uintptr_t> g_locked;  // [first page, end page) of each live CallLocks range
+std::atomic<long> g_locks_taken{0};        // (testing: ranges locked since start-up)
+
+constexpr uintptr_t kPage = 4096;
+uintptr_t page_lo(const void* p) { return reinterpret_cast<uintptr_t>(p) & ~(kPage - 1); }
+uintptr_t page_hi(const void* p, size_t n) {
+  return (reinterpret_cast<uintptr_t>(p) + n + kPage - 1) & ~(kPage - 1);
+}
+// (under g_lock_mu)
+bool touches_locked(uintptr_t lo, uintptr_t hi) {
+  auto it = g_locked.lower_bound(hi);  // the first range starting at or after hi
+  if (it == g_locked.begin()) return false;
+  --it;
+  return it->second > lo;
+}
+}  // namespace
+
+bool host_pinned(const void* p, size_t n) {
+  if (!p || n == 0) return false;
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  if (touches_locked(page_lo(p), page_hi(p, n))) return false;
+  return pinned_range(p, n);
+}
+
+int locked_ranges() {
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  return (int)g_locked.size();
+}
+
+long locks_taken() { return g_locks_taken.load(); }
+
 // ---- worker pool: concurrent jobs, one thread group per NUMA node ----
 //
-// Each job is a piece counter over fn(0) .. fn(pieces - 1).  Jobs from
+// Each job is a piece counter over fn(0) .. fn(pieces - 1), with a cap on the
+// pool workers that may join the caller on it (max_helpers).  Jobs from
 // different callers (host layers on different devices, or several sessions
 // of one device) run at the same time: a worker takes the next piece of the
-// oldest job of its own node, else of the oldest job of any node (no idle
-// worker while pieces are left), and the caller works on its own job too.
-// Sized from the CPUs the process may really use (usable_cores(): affinity
-// mask capped by the cgroup quota), split over the nodes in proportion to
-// their CPUs, each worker bound to its node's CPUs when there are several.
+// oldest job of its own node, else of the oldest job of any node, and the
+// caller works on its own job too.  Sized from the CPUs the process may
+// really use (usable_cores(): affinity mask capped by the cgroup quota),
+// split over the nodes in proportion to their CPUs, each worker bound to its
+// node's CPUs when there are several.
+//
+// CPU budget (round 5): a worker that finds nothing to take -- no job, or
+// only jobs whose pieces are all claimed or whose helper cap is reached --
+// spins at most spin_us() for the next publication, then sleeps until one.
+// A publication wakes at most as many sleepers as the job can use.  Round 4's
+// workers spun for as long as any job was published (every pool thread busy
+// for a whole staged call: ~5 ms of CPU per 16 MiB table).
 namespace {
 
 // set on the pool's threads, and on a caller while it works on its own job
@@ -84,46 +139,58 @@ struct Job {
   const std::function<void(size_t)>* fn;
   size_t pieces;
   int node;
+  int max_helpers;
   // (each counter on a cache line of its own: every thread of the job hits
   // next once per piece, finished once per piece, and the caller polls it)
   alignas(64) std::atomic<size_t> next{0};
   alignas(64) std::atomic<size_t> finished{0};
-  alignas(64) std::atomic<int> active{0};  // pieces in progress (testing: pool_take_peak_jobs)
+  alignas(64) std::atomic<int> helpers{0};  // workers that joined (at most max_helpers)
+  std::atomic<int> active{0};               // pieces in progress (testing: pool_take_peak_jobs)
 };
 
 // No lock on the way to a piece.  A job is published in a slot; a worker
 // takes it with a hazard pointer (its own slot says "I may touch this job",
-// then it re-reads the job slot), claims pieces with fetch_add and counts them
-// done with another; the caller unpublishes its job, then waits until every
-// piece is done and no worker's hazard names the job.  (The hazard is stored
-// before the job slot is re-read, the job slot cleared before the hazards are
-// read, all sequentially consistent: either the worker sees its job gone, or
-// the caller sees the worker's hazard.)  The mutex is only for sleeping.
+// then it re-reads the job slot), joins it if the helper cap allows, claims
+// pieces with fetch_add and counts them done with another; the caller
+// unpublishes its job, then waits until every piece is done and no worker's
+// hazard names the job.  (The hazard is stored before the job slot is
+// re-read, the job slot cleared before the hazards are read, all sequentially
+// consistent: either the worker sees its job gone, or the caller sees the
+// worker's hazard.)  The mutex is only for sleeping: a publication bumps gen_
+// and then reads sleepers_; a worker about to sleep counts itself in
+// sleepers_ and then re-reads gen_ (sequentially consistent, so one of the
+// two sees the other: no lost wake-up).
 // Round 4: with a mutex round trip per piece a parallel_for cost ~50 us; with
 // one per worker and job (pick and drop), 25-37 us of empty pieces on 16
-// threads (tools/ab/r4/pool_overhead.py) -- a 4 MiB staging copy took 0.047
-// ms where the bytes need ~0.024.
+// threads (tools/ab/r4/pool_overhead.py).
 class WorkPool {
  public:
   static constexpr int kJobSlots = 64;
   static constexpr int kMaxWorkers = 512;
 
-  void run(size_t pieces, const std::function<void(size_t)>& fn, int node) {
+  void run(size_t pieces, const std::function<void(size_t)>& fn, int node, int max_helpers) {
     start();
     Job j;
     j.fn = &fn;
     j.pieces = pieces;
     j.node = node;
+    j.max_helpers = max_helpers < 0 ? kMaxWorkers : max_helpers;
     int slot = -1;
-    for (int i = 0; i < kJobSlots && slot < 0; i++) {
-      Job* e = nullptr;
-      if (jobs_[i].compare_exchange_strong(e, &j)) slot = i;
-    }
+    if (j.max_helpers > 0)
+      for (int i = 0; i < kJobSlots && slot < 0; i++) {
+        Job* e = nullptr;
+        if (jobs_[i].compare_exchange_strong(e, &j)) slot = i;
+      }
     if (slot >= 0) {
-      published_.fetch_add(1);
-      if (sleepers_.load() > 0) {
-        std::lock_guard<std::mutex> l(mu_);
-        work_cv_.notify_all();
+      gen_.fetch_add(1);
+      const int sleeping = sleepers_.load();
+      if (sleeping > 0) {
+        // wake what the job can use beyond the workers already spinning
+        const int want = (int)std::min<size_t>(pieces - 1, (size_t)j.max_helpers) - spinning_.load();
+        if (want > 0) {
+          std::lock_guard<std::mutex> l(mu_);
+          for (int k = 0; k < std::min(want, sleeping); k++) work_cv_.notify_one();
+        }
       }
     }
     t_in_pool = true;
@@ -131,11 +198,15 @@ class WorkPool {
     t_in_pool = false;
     if (slot < 0) return;
     jobs_[slot].store(nullptr);  // (no worker takes it from here on)
-    published_.fetch_sub(1);
-    // the pieces still running elsewhere, and the workers that may still read j
+    // the pieces still running elsewhere (a spin of up to spin_us(), then
+    // short sleeps: a long piece does not cost the caller a core), and the
+    // workers that may still read j
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; j.finished.load(std::memory_order_acquire) != pieces; i++) {
       _mm_pause();
-      if ((i & 1023u) == 0) std::this_thread::yield();
+      if ((i & 63u) == 0 &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >= spin_us())
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     const int nw = nworkers_.load(std::memory_order_acquire);
     for (int w = 0; w < nw; w++)
@@ -172,8 +243,17 @@ class WorkPool {
       j->finished.fetch_add(1, std::memory_order_release);
     }
   }
-  // A published job with pieces left, preferring this node's: held by hazard
-  // slot w on return (nullptr: none).
+  // q (held by hazard slot w) has pieces left and room for one more helper:
+  // join it.
+  static bool join(Job* q) {
+    if (q->next.load(std::memory_order_relaxed) >= q->pieces) return false;
+    if (q->helpers.load(std::memory_order_relaxed) >= q->max_helpers) return false;
+    if (q->helpers.fetch_add(1) < q->max_helpers) return true;
+    q->helpers.fetch_sub(1);
+    return false;
+  }
+  // A published job this worker may join, preferring this node's: held by
+  // hazard slot w on return (nullptr: none).
   Job* take(int w, int node) {
     Job* any = nullptr;
     int any_i = -1;
@@ -181,20 +261,22 @@ class WorkPool {
       Job* q = jobs_[i].load(std::memory_order_acquire);
       if (!q) continue;
       hazard_[w].store(q);
-      if (jobs_[i].load() != q || q->next.load(std::memory_order_relaxed) >= q->pieces) {
+      if (jobs_[i].load() != q || q->next.load(std::memory_order_relaxed) >= q->pieces ||
+          q->helpers.load(std::memory_order_relaxed) >= q->max_helpers) {
         hazard_[w].store(nullptr);
         continue;
       }
-      if (q->node == node) return q;  // (held)
+      const bool mine = q->node == node;  // (read while the hazard holds q)
+      if (mine && join(q)) return q;      // (held)
       hazard_[w].store(nullptr);
-      if (!any) {
+      if (!any && !mine) {
         any = q;
         any_i = i;
       }
     }
     if (any) {  // another node's job: take it again under the hazard
       hazard_[w].store(any);
-      if (jobs_[any_i].load() == any && any->next.load(std::memory_order_relaxed) < any->pieces) return any;
+      if (jobs_[any_i].load() == any && join(any)) return any;
       hazard_[w].store(nullptr);
     }
     return nullptr;
@@ -226,13 +308,15 @@ class WorkPool {
     nworkers_.store(given, std::memory_order_release);
     started_.store(true, std::memory_order_release);
   }
-  // A worker that finds no job spins for spin_us() before it sleeps: a
-  // layer's chunks come every ~80 us, and a worker woken from sleep joins a
-  // 4 MiB staging copy late (profiles/r04/check3/timing.log).
+  // How long a worker that found nothing spins for the next publication
+  // before it sleeps (LSBM_POOL_SPIN_US, default 20): a staged table's four
+  // chunk copies come back to back, and a worker still spinning joins the
+  // next one at once; every microsecond of it is host CPU the database's own
+  // threads do not get.
   static double spin_us() {
     static const double us = [] {
       const char* v = getenv("LSBM_POOL_SPIN_US");
-      return v ? atof(v) : 100.0;
+      return v ? std::max(0.0, atof(v)) : 20.0;
     }();
     return us;
   }
@@ -240,34 +324,40 @@ class WorkPool {
     t_in_pool = true;
     NumaBind nb(bind ? node : -1, true, false);  // (kept bound for the thread's life)
     for (;;) {
-      if (published_.load(std::memory_order_acquire) == 0) {
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t i = 1; published_.load(std::memory_order_acquire) == 0; i++) {
-          _mm_pause();
-          if ((i & 255u) == 0 &&
-              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us()) {
-            std::unique_lock<std::mutex> l(mu_);
-            sleepers_.fetch_add(1);
-            work_cv_.wait(l, [&] { return published_.load() > 0; });
-            sleepers_.fetch_sub(1);
-            break;
-          }
-        }
-      }
+      const uint64_t g = gen_.load();  // (before the look: a later publication changes it)
       Job* j = take(w, node);
-      if (!j) {
-        _mm_pause();
+      if (j) {
+        work_on(j);
+        hazard_[w].store(nullptr);  // (j may be gone after this)
         continue;
       }
-      work_on(j);
-      hazard_[w].store(nullptr);  // (j may be gone after this)
+      idle(g);
     }
+  }
+  // Until a publication after generation g: a bounded spin, then sleep.
+  void idle(uint64_t g) {
+    spinning_.fetch_add(1);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool moved = false;
+    for (uint32_t i = 1; !(moved = gen_.load(std::memory_order_acquire) != g); i++) {
+      _mm_pause();
+      if ((i & 63u) == 0 &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >= spin_us())
+        break;
+    }
+    spinning_.fetch_sub(1);
+    if (moved) return;
+    std::unique_lock<std::mutex> l(mu_);
+    sleepers_.fetch_add(1);
+    work_cv_.wait(l, [&] { return gen_.load() != g; });
+    sleepers_.fetch_sub(1);
   }
   std::mutex mu_;  // start() and sleeping only
   std::condition_variable work_cv_;
   std::atomic<Job*> jobs_[kJobSlots] = {};
   std::atomic<Job*> hazard_[kMaxWorkers] = {};
-  std::atomic<int> published_{0}, sleepers_{0}, nworkers_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> sleepers_{0}, spinning_{0}, nworkers_{0};
   std::atomic<bool> started_{false};
   std::atomic<int> running_{0}, active_max_{0};
   std::atomic<bool> track_{false};
@@ -300,12 +390,26 @@ int max_sessions() {
 
 }  // namespace
 
-void parallel_for(size_t pieces, const std::function<void(size_t)>& fn) {
-  if (pieces == 1 || (pieces > 1 && t_in_pool)) {  // (nested: inline on this worker)
+void parallel_for(size_t pieces, const std::function<void(size_t)>& fn, int max_helpers) {
+  if (pieces == 1 || (pieces > 1 && (t_in_pool || max_helpers == 0))) {  // (nested: inline on this worker)
     for (size_t k = 0; k < pieces; k++) fn(k);
     return;
   }
-  if (pieces > 1) pool()->run(pieces, fn, t_job_node);
+  if (pieces > 1) pool()->run(pieces, fn, t_job_node, max_helpers);
+}
+
+// One thread copies ~50 GB/s into pinned staging with non-temporal stores
+// (profiles/r04/check18/one_auto_p1.log:3) and PCIe takes ~56 GB/s: the caller
+// and 3 workers keep the copy well ahead of the DMA (LSBM_COPY_THREADS, the
+// threads in all, caller included).  Round 4 used every pool thread (a 170
+// GB/s burst for the first 4 MiB share, and every core of the quota busy).
+int copy_helpers() {
+  static const int n = [] {
+    const char* v = getenv("LSBM_COPY_THREADS");
+    const int t = v ? atoi(v) : 4;
+    return std::max(0, std::min(t > 0 ? t : 4, pool()->threads() + 1) - 1);
+  }();
+  return n;
 }
 
 int pool_threads() { return pool()->threads(); }
@@ -352,9 +456,8 @@ void stream_copy(char* d, const char* s, size_t n) {
 }
 }  // namespace
 
-// Pieces of about n / (2 (workers + 1)), at least 128 KiB, 4 KiB multiples:
-// every worker gets a share of a 4 MiB chunk (round 3's fixed 1 MiB pieces
-// left 12 of 16 threads idle on one table's 4 MiB chunks: 47 GB/s).
+// Pieces of about n / (2 (helpers + 1)), at least 128 KiB, 4 KiB multiples,
+// over the caller and copy_helpers() workers.
 void parallel_copy(void* dst, const void* src, size_t n) {
   char* d = static_cast<char*>(dst);
   const char* s = static_cast<const char*>(src);
@@ -363,12 +466,16 @@ void parallel_copy(void* dst, const void* src, size_t n) {
     stream_copy(d, s, n);
     return;
   }
-  const size_t ways = 2 * ((size_t)pool_threads() + 1);
+  const int helpers = copy_helpers();
+  const size_t ways = 2 * ((size_t)helpers + 1);
   const size_t piece = std::max(kMinPiece, ((n + ways - 1) / ways + 4095) / 4096 * 4096);
-  parallel_for((n + piece - 1) / piece, [&](size_t k) {
-    const size_t off = k * piece;
-    stream_copy(d + off, s + off, std::min(piece, n - off));
-  });
+  parallel_for(
+      (n + piece - 1) / piece,
+      [&](size_t k) {
+        const size_t off = k * piece;
+        stream_copy(d + off, s + off, std::min(piece, n - off));
+      },
+      helpers);
 }
 
 // ---- per-call page locks ----
@@ -390,6 +497,11 @@ bool CallLocks::add(int device, const void* p, size_t n, bool writable) {
   }
   const bool ro = __atomic_load_n(&read_only[device], __ATOMIC_RELAXED) == 1;
   if (!ro && !writable) return false;
+  const uintptr_t lo = page_lo(p), hi = page_hi(p, n);
+  // check -> register -> resolve -> (unregister) as one step against every
+  // other call's locks (g_lock_mu: ~1 us of registration per table)
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  if (touches_locked(lo, hi)) return false;  // (another live call's pages: staged)
   // Never over a registration the caller made: HIP accepts a range whose
   // first page is registered already, and unregistering such a range can
   // break the older one (a crash in a later call, found by table_gpu_test).
@@ -411,18 +523,25 @@ bool CallLocks::add(int device, const void* p, size_t n, bool writable) {
   // but HIP then resolves its first byte to the older one, and an async DMA of
   // the whole range fails: only a range that now resolves as one buffer from
   // end to end counts (the staging copy takes the rest).
-  if (!host_pinned(p, n)) {
+  if (!pinned_range(p, n)) {
     (void)hipHostUnregister(q);
     (void)hipGetLastError();
     return false;
   }
-  regs_.push_back(q);
+  g_locked.emplace(lo, hi);
+  regs_.push_back(Reg{q, lo});
+  g_locks_taken.fetch_add(1);
   return true;
 }
 
 CallLocks::~CallLocks() {
-  for (void* q : regs_) (void)hipHostUnregister(q);
-  if (!regs_.empty()) (void)hipGetLastError();
+  if (regs_.empty()) return;
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  for (const Reg& r : regs_) {
+    (void)hipHostUnregister(r.p);
+    g_locked.erase(r.lo);
+  }
+  (void)hipGetLastError();
 }
 
 // ---- buffers ----
@@ -444,43 +563,97 @@ static size_t with_headroom(size_t bytes) {
   return (bytes + bytes / 4 + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
 }
 
+// Page-locked bytes held by each device's sessions, and the budget above which
+// a released lease trims the idle sessions' staging (LSBM_PINNED_MB per
+// device, default 1024): up to 8 sessions x 4 stages of compaction-sized
+// buffers (~80 MiB each) would otherwise pin ~2.5 GiB per device until
+// shutdown.  A failed allocation trims every idle session of the
+// device and tries once more before the call fails.
+namespace {
+std::atomic<size_t> g_pinned[kMaxDevices];
+
+size_t pinned_budget() {
+  static const size_t b = [] {
+    const char* v = getenv("LSBM_PINNED_MB");
+    const long mb = v ? atol(v) : 1024;
+    return (size_t)std::max(0L, mb) << 20;
+  }();
+  return b;
+}
+
+void count_pinned(int device, long long delta) {
+  if (device >= 0 && device < kMaxDevices) g_pinned[device].fetch_add((size_t)delta);
+}
+
+// Frees the staging of the device's idle sessions but the `keep` most
+// recently released (under g_reg; an idle session has no work in flight:
+// its lease drained every stage).
+void trim_idle_locked(int device, size_t keep) {
+  DeviceSessions& ds = g_sessions[device];
+  for (size_t i = 0; i + keep < ds.idle.size(); i++) ds.idle[i]->release_staging();
+}
+}  // namespace
+
+size_t pinned_bytes(int device) {
+  return device >= 0 && device < kMaxDevices ? g_pinned[device].load() : 0;
+}
+
+hipError_t StagePair::alloc(size_t bytes, bool map) {
+  bytes = with_headroom(bytes);
+  hipError_t e = hipSuccess;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if (attempt) {  // (pinned or device memory ran out: give back the idle sessions' staging)
+      if (device < 0 || device >= kMaxDevices) break;
+      std::lock_guard<std::mutex> l(g_reg);
+      trim_idle_locked(device, 0);
+    }
+    e = host_alloc(reinterpret_cast<void**>(&h), bytes,
+                   map ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault, node);
+    if (e == hipSuccess) {
+      count_pinned(device, (long long)bytes);
+      cap = bytes;  // (release() uncounts it from here on)
+      mapped = map;
+      e = map ? hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0)
+              : hipMalloc(reinterpret_cast<void**>(&d), bytes);
+    }
+    if (e == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    release();
+  }
+  return e;
+}
+
 hipError_t StagePair::reserve(size_t bytes) {
   if (bytes <= cap && !mapped) return hipSuccess;
   release();
-  bytes = with_headroom(bytes);
-  hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault, node);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), bytes);
-  mapped = false;
-  if (e != hipSuccess) {
-    release();
-    return e;
-  }
-  cap = bytes;
-  return hipSuccess;
+  return alloc(bytes, false);
 }
 
 hipError_t StagePair::reserve_mapped(size_t bytes) {
   if (bytes <= cap && mapped) return hipSuccess;
   release();
-  bytes = with_headroom(bytes);
-  hipError_t e = host_alloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocMapped | hipHostMallocCoherent, node);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0);
-  if (e != hipSuccess) {
-    if (h) (void)hipHostFree(h);
-    h = d = nullptr;
-    return e;
-  }
-  mapped = true;
-  cap = bytes;
-  return hipSuccess;
+  return alloc(bytes, true);
 }
 
 void StagePair::release() {
-  if (h) (void)hipHostFree(h);
+  if (h) {
+    (void)hipHostFree(h);
+    count_pinned(device, -(long long)cap);
+  }
   if (d && !mapped) (void)hipFree(d);
   h = d = nullptr;
   cap = 0;
   mapped = false;
+}
+
+void HostSession::release_staging() {
+  DeviceGuard g(device_);
+  for (Stage& s : stage_) {
+    s.bulk.release();
+    s.meta.release();
+    s.res.release();
+    s.zmeta.release();
+  }
 }
 
 // ---- session ----
@@ -488,6 +661,7 @@ hipError_t HostSession::init() {
   node_ = device_numa_node(device_);
   for (Stage& s : stage_) {
     s.bulk.node = s.meta.node = s.res.node = s.zmeta.node = node_;
+    s.bulk.device = s.meta.device = s.res.device = s.zmeta.device = device_;
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming);
@@ -654,9 +828,10 @@ SessionLease::~SessionLease() {
     std::lock_guard<std::mutex> l(g_reg);
     DeviceSessions& ds = g_sessions[s_->device()];
     ds.idle.push_back(s_);
+    if (pinned_bytes(s_->device()) > pinned_budget()) trim_idle_locked(s_->device(), 1);
     ds.cv.notify_all();
   }
-  t_job_node = prev_node_;
+  if (node_set_) t_job_node = prev_node_;  // (only what Open set: an outer lease's node stays)
   delete guard_;
 }
 
@@ -726,6 +901,7 @@ Status SessionLease::Open(int device) {
   }
   s_ = s;
   prev_node_ = t_job_node;
+  node_set_ = true;
   t_job_node = s->node();
   return Status::OK();
 }
@@ -767,7 +943,8 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_overlap(int
 }
 
 // Testing: `callers` threads each run `jobs` parallel_for jobs of 1..max_pieces
-// pieces (some nested: a piece that runs its own parallel_for, inline), each
+// pieces (helper caps from none to 3 or any; some nested: a piece that runs
+// its own parallel_for, inline), each
 // piece adding 1 to its own counter; returns the number of counters that
 // are not exactly 1 afterwards (0: every piece of every job ran once).
 extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_stress(int callers, int jobs, int max_pieces) {
@@ -783,14 +960,18 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_stress(int 
         std::vector<std::atomic<int>> hit(n);
         for (auto& h : hit) h.store(0);
         const bool nested = (x >> 40) % 5 == 0;
-        lsbm::parallel_for(n, [&](size_t k) {
-          if (nested) {
-            std::atomic<int> inner{0};
-            lsbm::parallel_for(3, [&](size_t) { inner.fetch_add(1); });
-            if (inner.load() != 3) hit[k].fetch_add(100);
-          }
-          hit[k].fetch_add(1);
-        });
+        const int cap = (int)((x >> 20) % 5) - 1;  // helper caps -1 (any) .. 3
+        lsbm::parallel_for(
+            n,
+            [&](size_t k) {
+              if (nested) {
+                std::atomic<int> inner{0};
+                lsbm::parallel_for(3, [&](size_t) { inner.fetch_add(1); });
+                if (inner.load() != 3) hit[k].fetch_add(100);
+              }
+              hit[k].fetch_add(1);
+            },
+            cap);
         for (auto& h : hit) bad += h.load() != 1;
       }
     });
@@ -810,4 +991,32 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_host_copy(void* 
 
 extern "C" __attribute__((visibility("default"))) int lsbm_test_host_pinned(const void* p, size_t n) {
   return lsbm::host_pinned(p, n) ? 1 : 0;
+}
+
+// Testing: how many distinct threads ran the pieces of one capped job.
+extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_helpers(int pieces, int piece_us,
+                                                                         int max_helpers) {
+  if (pieces <= 0 || piece_us < 0) return -1;
+  std::mutex mu;
+  std::vector<std::thread::id> ids;
+  lsbm::parallel_for(
+      (size_t)pieces,
+      [&](size_t) {
+        {
+          std::lock_guard<std::mutex> l(mu);
+          if (std::find(ids.begin(), ids.end(), std::this_thread::get_id()) == ids.end())
+            ids.push_back(std::this_thread::get_id());
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(piece_us));
+      },
+      max_helpers);
+  return (int)ids.size();
+}
+
+extern "C" __attribute__((visibility("default"))) int lsbm_test_locked_ranges(void) {
+  return lsbm::locked_ranges();
+}
+
+extern "C" __attribute__((visibility("default"))) long lsbm_test_locks_taken(void) {
+  return lsbm::locks_taken();
 }

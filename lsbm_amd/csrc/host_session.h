@@ -65,10 +65,14 @@ struct StagePair {
   uint8_t* d = nullptr;
   size_t cap = 0;
   bool mapped = false;
-  int node = -1;  // NUMA node of the host pages (-1: HIP's default placement)
+  int node = -1;    // NUMA node of the host pages (-1: HIP's default placement)
+  int device = -1;  // the session's device (pinned-bytes accounting)
   hipError_t reserve(size_t bytes);  // grows (never shrinks); contents are not kept
   hipError_t reserve_mapped(size_t bytes);
   void release();
+
+ private:
+  hipError_t alloc(size_t bytes, bool map);
 };
 
 // One pipeline stage.
@@ -136,6 +140,8 @@ class HostSession {
 
   // Frees every session (lsbm_crc32c_shutdown).
   static void ShutdownAll();
+  // Frees this (idle) session's staging buffers; they grow again on demand.
+  void release_staging();
 
  private:
   friend class SessionLease;
@@ -171,12 +177,18 @@ class SessionLease {
   HostSession* s_ = nullptr;
   DeviceGuard* guard_ = nullptr;
   int prev_node_ = -1;
+  bool node_set_ = false;  // Open got as far as steering this thread's jobs
 };
 
-// Sessions created so far for `device` (idle or leased).
+// Sessions created so far for `device` (idle or leased), and the page-locked
+// staging bytes they hold (kept under LSBM_PINNED_MB per device, default
+// 1024, by trimming idle sessions when a lease is released).
 int session_count(int device);
+size_t pinned_bytes(int device);
 
-// Is [p, p + n) inside page-locked host memory (hipHostMalloc'd or registered)?
+// Is [p, p + n) inside page-locked host memory (hipHostMalloc'd or registered)
+// that stays locked for the caller's call?  Not if a page of it is held by
+// another call's CallLocks (that call unlocks it when it returns).
 bool host_pinned(const void* p, size_t n);
 
 // Page-locks a call's pageable images (hipHostRegister: ~1 us, the pages are
@@ -187,6 +199,10 @@ bool host_pinned(const void* p, size_t n);
 // (hipHostRegisterReadOnly where the device supports it, so read-only
 // mappings such as an mmap'd table file qualify; else only images the caller
 // passed as writable).  LSBM_AUTO_LOCK=0 turns it off (staging copies).
+// Thread-safe: registrations and unregistrations of all calls are serialised
+// under one process-wide mutex, and a range that shares a page with another
+// live call's lock is neither locked nor taken as page-locked (host_pinned):
+// concurrent callers whose images are neighbours on the heap stage instead.
 class CallLocks {
  public:
   CallLocks() = default;
@@ -194,28 +210,43 @@ class CallLocks {
   CallLocks& operator=(const CallLocks&) = delete;
   ~CallLocks();
   // true when [p, p + n) is page-locked for this call from here on (false: it
-  // could not be, e.g. a page of it is registered already; nothing changed)
+  // could not be, e.g. a page of it is registered already or held by another
+  // call's lock; nothing changed)
   bool add(int device, const void* p, size_t n, bool writable);
   static bool enabled();
 
  private:
-  std::vector<void*> regs_;
+  struct Reg {
+    void* p;
+    uintptr_t lo;  // its first page (the key of its range in the lock set)
+  };
+  std::vector<Reg> regs_;
 };
+
+// Page ranges held by live CallLocks, and ranges locked since start-up (testing).
+int locked_ranges();
+long locks_taken();
 
 // fn(0) ... fn(pieces - 1) over the worker pool and the caller; returns when
 // all have run.  The pool has usable_cores() - 1 threads (the affinity mask
 // capped by the cgroup CPU quota), grouped by NUMA node; jobs of concurrent
 // callers run at the same time, each worker preferring jobs of its own node
-// (the caller's session's device node).  A call from inside a pool task runs
-// its pieces inline on that thread (no deadlock, no extra parallelism).
-void parallel_for(size_t pieces, const std::function<void(size_t)>& fn);
+// (the caller's session's device node).  At most max_helpers workers join
+// the caller (-1: any; 0: the caller alone).  A call from inside a pool task
+// runs its pieces inline on that thread (no deadlock, no extra parallelism).
+// Idle workers spin at most LSBM_POOL_SPIN_US (20 us) and then sleep.
+void parallel_for(size_t pieces, const std::function<void(size_t)>& fn, int max_helpers = -1);
 
 // The pool's worker count (starts it), and, for tests, the most jobs that
 // had pieces running at the same moment since the previous call.
 int pool_threads();
 int pool_take_peak_jobs();
 
-// memcpy of n bytes, split over the worker pool when n >= 4 MiB.
+// Workers that join a staging copy (LSBM_COPY_THREADS - 1; default 3).
+int copy_helpers();
+
+// memcpy of n bytes into pinned staging (non-temporal stores), split over the
+// caller and copy_helpers() workers when n >= 256 KiB.
 void parallel_copy(void* dst, const void* src, size_t n);
 
 // Diagnostics (LSBM_HOST_TIMING=1 in the environment): a layer's pipeline

@@ -276,7 +276,7 @@ bool run_small_locked(HostSession& hs, const TableImage* tables, size_t count, O
 // The pipeline.  Seal: trailers written into the host images.  Verify: ok[]
 // per block, concatenated over the tables in their block order.
 Status run(int device, const TableImage* tables, size_t count, Op op, std::vector<uint8_t>* ok_out,
-           size_t* nbad_out) {
+           size_t* nbad_out, bool writable) {
   HostTiming tm(op == Op::kSeal ? "SealTables" : "VerifyTables");
   Plan plan;
   make_plan(tables, count, &plan);
@@ -299,12 +299,16 @@ Status run(int device, const TableImage* tables, size_t count, Op op, std::vecto
     // (profiles/r04/check17/, seal_register_per_call vs seal_pageable).
     // Big jobs keep the staging pipeline (53.8 against 51.3 GB/s in place,
     // profiles/r04/check13/host_*.log).
+    // Verify too, for writable images (lsbm's ReadBlock buffers are heap
+    // memory, table/format.cc:79-82): 0.35 ms and ~0.4 ms of host CPU per
+    // 16 MiB table against 0.41 ms and ~5 ms through round 4's staging
+    // (DESIGN section 5).
     // (not for zero copy: its seal stores into the image, and a read-only
     // registration must never be written by the device)
     if (total <= zero_copy_max() && CallLocks::enabled() && !small_locked_zero_copy())
       for (size_t t = 0; t < count; t++)
         if (!pinned[t] && tables[t].n != 0)
-          pinned[t] = locks.add(device, tables[t].file, tables[t].file_size, op == Op::kSeal);
+          pinned[t] = locks.add(device, tables[t].file, tables[t].file_size, writable);
     bool all_pinned = true;
     for (size_t t = 0; t < count; t++) all_pinned = all_pinned && (tables[t].n == 0 || pinned[t]);
     if (all_pinned && total <= zero_copy_max() &&
@@ -476,10 +480,11 @@ Status SealTables(int device, const TableImage* tables, size_t count) {
     Status s = check_handles(tb.file_size, tb.handles, tb.n);
     if (!s.ok()) return s;
   }
-  return run(device, tables, count, Op::kSeal, nullptr, nullptr);
+  return run(device, tables, count, Op::kSeal, nullptr, nullptr, true);
 }
 
-Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok) {
+Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok,
+                    ImageMemory memory) {
   size_t total = 0;
   for (size_t t = 0; t < count; t++) total += tables[t].n;
   if (ok) ok->assign(total, 1);
@@ -491,9 +496,13 @@ Status VerifyTables(int device, const TableImage* tables, size_t count, std::vec
     if (!s.ok()) return s;
   }
   size_t nbad = 0;
-  Status s = run(device, tables, count, Op::kVerify, ok, &nbad);
+  Status s = run(device, tables, count, Op::kVerify, ok, &nbad, memory == kImagesWritable);
   if (!s.ok()) return s;
   return nbad ? Status::Corruption("block checksum mismatch") : Status::OK();
+}
+
+Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok) {
+  return VerifyTables(device, tables, count, ok, kImagesReadOnly);
 }
 
 Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
@@ -504,13 +513,25 @@ Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* h
   return SealTables(device, &t, 1);
 }
 
-Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
-                    size_t n, std::vector<uint8_t>* ok) {
+namespace {
+Status verify_one(int device, char* file, size_t file_size, const BlockHandle* handles, size_t n,
+                  std::vector<uint8_t>* ok, ImageMemory memory) {
   if (ok) ok->assign(n, 1);
   if (n == 0) return Status::OK();
   if (!file || !handles) return Status::InvalidArgument("null pointer");
-  const TableImage t{const_cast<char*>(file), file_size, handles, nullptr, n};
-  return VerifyTables(device, &t, 1, ok);
+  const TableImage t{file, file_size, handles, nullptr, n};
+  return VerifyTables(device, &t, 1, ok, memory);
+}
+}  // namespace
+
+Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
+                    size_t n, std::vector<uint8_t>* ok) {
+  return verify_one(device, const_cast<char*>(file), file_size, handles, n, ok, kImagesReadOnly);
+}
+
+Status VerifyBlocks(int device, char* file, size_t file_size, const BlockHandle* handles, size_t n,
+                    std::vector<uint8_t>* ok) {
+  return verify_one(device, file, file_size, handles, n, ok, kImagesWritable);
 }
 
 }  // namespace lsbm

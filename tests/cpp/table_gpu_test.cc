@@ -3,6 +3,7 @@
 // TableBuilder::WriteRawBlock (table/table_builder.cc:245-249) and ReadBlock
 // (table/format.cc:95-103), computed with util/crc32c.h.  Needs a GPU.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -210,6 +211,26 @@ int main() {
       close(fd);
       unlink(path);
     }
+
+    // the same table from heap memory, as lsbm's ReadBlock holds it (pread
+    // into new char[], table/format.cc:79-82): a writable char* image is
+    // page-locked for the call and DMA-ed in place (one more per-call lock),
+    // the same bytes as const char* are not (staged), and both verify
+    const char* al = getenv("LSBM_AUTO_LOCK");
+    const char* sl = getenv("LSBM_SMALL_LOCKED");
+    const bool locks_on = !(al && atoi(al) == 0) && !(sl && strcmp(sl, "zc") == 0);
+    const long l0 = lsbm_test_locks_taken();
+    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1);
+    EXPECT(st.ok() && std::count(ok1.begin(), ok1.end(), 1) == (long)h[1].size());
+    const long l1 = lsbm_test_locks_taken();
+    EXPECT(l1 == l0 + (locks_on ? 1 : 0));
+    st = lsbm::VerifyBlocks(0, static_cast<const char*>(&f[1][0]), f[1].size(), h[1].data(), h[1].size(), &ok1);
+    EXPECT(st.ok() && lsbm_test_locks_taken() == l1);
+    f[1][h[1][6].offset + 2] ^= 0x02;
+    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1);
+    EXPECT(st.IsCorruption() && std::count(ok1.begin(), ok1.end(), 0) == 1 && ok1[6] == 0);
+    f[1][h[1][6].offset + 2] ^= 0x02;
+    EXPECT(lsbm_test_locked_ranges() == 0);
   }
 
   fprintf(stderr, "section: page locks next to the caller's registrations\n");

@@ -472,6 +472,41 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb
     assert speedup >= (1.1 if pinned == 0 and auto_lock == "0" else 0.95), r.stdout
 
 
+@pytest.mark.parametrize("auto_lock", ["1", "0"], ids=["auto-lock", "staged"])
+def test_cpp_concurrent_callers_on_shared_pages(torch_cuda, oracle, tmp_path, auto_lock):
+    """8 threads seal and verify (writable char*, page-locked per call) small
+    pageable table images packed back to back in ONE allocation, so that
+    neighbours share pages, over 6 rounds of shuffled call orders
+    (tests/cpp/shared_page_seal_test.cc): every trailer equals the oracle's
+    WriteRawBlock trailer and nothing else changed, every verify passes and a
+    flipped byte fails exactly its block, no per-call lock outlives its call,
+    and later serial and whole-batch calls on the same memory still succeed
+    (the per-call locks' check -> register -> unregister
+    is serialised against every other call's locks)."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "shared_page_seal_test"
+    libdir = os.path.join(repo, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(repo, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(repo, "tests", "cpp", "shared_page_seal_test.cc"), "-L", libdir,
+                    "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64", "-ldl",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    env = dict(os.environ, LSBM_AUTO_LOCK=auto_lock)
+    r = subprocess.run([str(exe), os.path.join(repo, "oracle", "liboracle_crc32c.so"), "8", "192", "6"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK"), r.stdout
+    fields = dict(kv.split("=") for kv in r.stdout.split()[1:])
+    assert int(fields["shared_pages"]) > 100
+    if auto_lock == "1":
+        assert int(fields["locked_calls"]) > 0  # (some calls did lock their pages)
+    else:
+        assert int(fields["locked_calls"]) == 0
+
+
 def test_level2_binding_over_the_reference_table_code(torch_cuda):
     """integration/leveldb_gpu_checksum.h, linked with the reference's own
     table/ and util/ objects (oracle/Makefile gpubind, built in the build

@@ -3,8 +3,10 @@ its own two ranks (torch.distributed.run as a child process), each rank
 checksums its own config-5 shard on the HIP path: global blocks [10M r,
 10M (r + 1)) of the one 80M x 4 KiB dataset (BASELINE.json configs[4]; block i
 = bytes [4096 i, 4096 (i + 1)) of the splitmix64 stream 0x5EED0000), and the
-per-rank results are checked here against the oracle by global block index.  Both ranks share the one MI355X (LSBM_BENCH_DEVICES=1) and meet
-over gloo (LSBM_BENCH_BACKEND=gloo); the driver's 8-GPU run uses RCCL."""
+per-rank results are checked here against the oracle by global block index.
+Both ranks share the one MI355X (LSBM_BENCH_DEVICES=1) and meet over bench.py's
+DEFAULT backend (gloo on CPU tensors for the barrier and the MAX of the elapsed
+time: no RCCL anywhere), the same code the driver's 8-GPU run executes."""
 import glob
 import json
 import os
@@ -22,8 +24,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
     env = {k: v for k, v in os.environ.items()
-           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
-    env.update(LSBM_BENCH_DEVICES="1", LSBM_BENCH_BACKEND="gloo")
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                        "LSBM_BENCH_BACKEND")}
+    env.update(LSBM_BENCH_DEVICES="1")
     prefix = str(tmp_path / "samples")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
                         "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
@@ -35,6 +38,7 @@ def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["blocks_per_gpu"] == 10_000_000
+    assert "over gloo" in line["config"]["parallelism"]  # the default: no RCCL in the harness
     files = sorted(glob.glob(prefix + ".rank*.npz"))
     assert len(files) == 2
     seen = []

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -86,9 +87,16 @@ int check_table(const Table& t) {
 
 struct CpuStat {
   long long periods = -1, throttled = -1, throttled_us = -1, usage_us = -1;
+  double proc_s = 0;  // this process's CPU time, all threads (getrusage)
 };
+double proc_cpu_s() {
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
 CpuStat read_cpu_stat() {
   CpuStat c;
+  c.proc_s = proc_cpu_s();
   FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
   if (!f) return c;
   char key[64];
@@ -134,10 +142,97 @@ void print_phase(const char* what, const std::vector<double>& v, double bytes, c
   double slow_at = -1;  // the slowest call's start, ms after the process's first layer call
   if (!starts.empty())
     slow_at = (starts[std::max_element(v.begin(), v.end()) - v.begin()] - g_t_first) * 1e3;
-  printf("{\"what\": \"%s\", \"bytes\": %.0f, \"dist\": %s, \"slowest_at_ms\": %.1f, \"cpu_stat\": {\"nr_periods\": %lld, "
+  // host CPU per call: this process's CPU time (every thread: the caller,
+  // the pool's workers, HIP's own) over the phase, divided by its calls
+  printf("{\"what\": \"%s\", \"bytes\": %.0f, \"dist\": %s, \"slowest_at_ms\": %.1f, "
+         "\"host_cpu_ms_per_call\": %.3f, \"cpu_stat\": {\"nr_periods\": %lld, "
          "\"nr_throttled\": %lld, \"throttled_ms\": %.3f, \"cpu_ms\": %.1f}, \"status\": \"%s\", \"bad\": %d}\n",
-         what, bytes, dist_json(v, bytes).c_str(), slow_at, b.periods - a.periods, b.throttled - a.throttled,
-         (b.throttled_us - a.throttled_us) / 1e3, (b.usage_us - a.usage_us) / 1e3, status, bad);
+         what, bytes, dist_json(v, bytes).c_str(), slow_at, v.empty() ? 0.0 : (b.proc_s - a.proc_s) * 1e3 / v.size(),
+         b.periods - a.periods, b.throttled - a.throttled, (b.throttled_us - a.throttled_us) / 1e3,
+         (b.usage_us - a.usage_us) / 1e3, status, bad);
+  fflush(stdout);
+}
+
+// A CPU-bound co-runner's unit of work: xorshift steps (no memory traffic).
+uint64_t spin_work(uint64_t iters, uint64_t seed) {
+  uint64_t x = seed | 1;
+  for (uint64_t i = 0; i < iters; i++) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+  }
+  return x;
+}
+double thread_cpu_s() {
+  struct rusage ru;
+  getrusage(RUSAGE_THREAD, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
+int usable_cores_guess() { return lsbm_host_threads() + 1; }
+volatile uint64_t g_sink;
+
+// k co-runner threads each do a fixed amount of CPU-bound work (calibrated to
+// ~ the time of 100 calls), alone and then while this thread makes layer
+// calls back to back; prints the co-runners' slowdown and the layer's own
+// host CPU per call (the process's CPU time less the co-runners').
+void corunner_phase(const char* what, const std::function<lsbm::Status()>& call, int k) {
+  // the call's time, and the work that takes 100 of them on one core
+  const double c0 = now();
+  for (int i = 0; i < 10; i++) (void)call();
+  const double per_call = (now() - c0) / 10;
+  const double w0 = now();
+  g_sink = spin_work(20000000, 1);
+  const double per_iter = (now() - w0) / 20000000;
+  const uint64_t iters = (uint64_t)(100 * per_call / per_iter);
+  auto run_corunners = [&](bool beside, double* wall_max, double* cpu_sum, int* calls) {
+    std::atomic<int> left{k};
+    std::vector<double> wall(k), cpu(k);
+    std::vector<std::thread> th;
+    std::atomic<bool> go{false};
+    for (int j = 0; j < k; j++)
+      th.emplace_back([&, j] {
+        while (!go.load()) std::this_thread::yield();
+        const double t0 = now(), u0 = thread_cpu_s();
+        g_sink = spin_work(iters, j + 2);
+        wall[j] = now() - t0;
+        cpu[j] = thread_cpu_s() - u0;
+        left--;
+      });
+    go.store(true);
+    int n = 0;
+    if (beside)
+      while (left.load() > 0) {
+        (void)call();
+        n++;
+      }
+    for (auto& x : th) x.join();
+    *wall_max = *std::max_element(wall.begin(), wall.end());
+    *cpu_sum = 0;
+    for (double c : cpu) *cpu_sum += c;
+    *calls = n;
+  };
+  std::vector<double> alone, beside, layer_cpu;
+  int calls = 0;
+  for (int rep = 0; rep < 5; rep++) {
+    double wmax, csum;
+    int n;
+    run_corunners(false, &wmax, &csum, &n);
+    alone.push_back(wmax);
+    const double p0 = proc_cpu_s();
+    run_corunners(true, &wmax, &csum, &n);
+    beside.push_back(wmax);
+    layer_cpu.push_back(n ? (proc_cpu_s() - p0 - csum) / n : 0.0);
+    calls += n;
+  }
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  printf("{\"what\": \"corunner_%s\", \"corunner_threads\": %d, \"call_ms\": %.3f, \"alone_ms\": %.2f, "
+         "\"beside_ms\": %.2f, \"slowdown_pct\": %.2f, \"calls\": %d, \"layer_cpu_ms_per_call\": %.3f, "
+         "\"pool_threads\": %d}\n",
+         what, k, per_call * 1e3, med(alone) * 1e3, med(beside) * 1e3, 100 * (med(beside) / med(alone) - 1), calls,
+         med(layer_cpu) * 1e3, lsbm_host_threads());
   fflush(stdout);
 }
 
@@ -223,6 +318,23 @@ int main(int argc, char** argv) {
     } else {
       if (!phase(("seal" + sfx).c_str(), [&] { return seal(t); })) return 1;
       if (!phase(("verify" + sfx).c_str(), [&] { return verify(t); })) return 1;
+    }
+    if (!locked) {
+      // The same bytes as const char* (a read-only mapping, for all the layer
+      // knows): staged through pinned buffers; and what the layer's calls cost
+      // a CPU-bound co-runner.
+      auto verify_const = [&](Table& tb) {
+        return lsbm::VerifyBlocks(0, static_cast<const char*>(tb.img.data()), tb.img.size(), tb.h.data(),
+                                  tb.h.size(), &ok);
+      };
+      if (!phase("verify_pageable_const_staged", [&] { return verify_const(t); })) return 1;
+      corunner_phase("verify_const_staged", [&] { return verify_const(t); }, 1);
+      corunner_phase("verify_heap_locked", [&] { return verify(t); }, 1);
+      corunner_phase("seal_pageable_locked", [&] { return seal(t); }, 1);
+      const int all_but_one = std::max(1, usable_cores_guess() - 1);
+      corunner_phase("verify_const_staged", [&] { return verify_const(t); }, all_but_one);
+      corunner_phase("verify_heap_locked", [&] { return verify(t); }, all_but_one);
+      corunner_phase("seal_pageable_locked", [&] { return seal(t); }, all_but_one);
     }
     if (!locked) {
       // seal and verify alternating: is the seal's tail the order it runs in?
