@@ -524,6 +524,31 @@ def test_level2_binding_over_the_reference_table_code(torch_cuda):
     assert r.stdout.startswith("OK"), r.stdout
 
 
+def test_gpu_sealed_table_builder_matches_the_reference_table_builder(torch_cuda):
+    """integration/gpu_table_builder.h over the reference's own BlockBuilder,
+    FilterBlockBuilder, BlockHandle / Footer and comparators (oracle/Makefile
+    gputable, built in the build container): compaction-shaped internal-key
+    streams (db_bench user keys, 100-B values) cut into 16 MiB tables with a
+    bloom filter, lsbm's default 8 MiB with none, 16 KiB blocks with snappy
+    requested, a 37-entry and an empty table.  Each table's trailers are
+    reserved and sealed by ONE SealBlocks call at Finish (page-locked in place),
+    and the file is byte-identical to the unmodified TableBuilder's (whose
+    trailers come from the reference's own util/crc32c.cc, block by block); the
+    reference's Table::Open / ReadBlock with verify_checksums reads every entry
+    back.  Skipped where the binary was not built."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                       "gpu_table_builder")
+    if not os.access(exe, os.X_OK):
+        pytest.skip("oracle/_ref/gpu_table_builder not built (needs /root/reference at build time)")
+    r = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "FAIL" not in r.stdout and r.stdout.strip().splitlines()[-1].startswith("OK"), r.stdout
+    assert r.stdout.count("identical=1") == 3 + 3 + 3 + 1 + 1
+
+
 def test_cpp_block_compression_layer(torch_cuda, tmp_path):
     """include/lsbm/block_compression.h from C++: WriteBlock's compression and
     12.5% rule against the snappy oracle, ReadBlock's decompression and its

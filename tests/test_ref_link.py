@@ -57,3 +57,25 @@ def test_level2_binding_compiles_and_links_against_the_reference():
     assert os.access(exe, os.X_OK)
     ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
     assert "liblsbm_crc32c.so" in ldd and "libamdhip64" in ldd
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "table")), reason="needs /root/reference")
+def test_gpu_table_builder_compiles_and_links_against_the_reference():
+    """integration/gpu_table_builder.h (the reference's TableBuilder with its
+    trailers reserved and sealed by one SealBlocks call per table) compiled
+    with the reference's own headers and linked with its table/, util/ and
+    common/ objects plus its own util/crc32c.cc and util/hash.cc (oracle/Makefile
+    gputable): the unmodified TableBuilder in the binary takes Extend and Hash
+    from the reference's sources, the GPU builder SealBlocks from the library.
+    tests/test_gpu_parity.py runs it on the GPU."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "gputable"], check=True)
+    exe = os.path.join(REPO, "oracle", "_ref", "gpu_table_builder")
+    assert os.access(exe, os.X_OK)
+    syms = subprocess.run(["nm", exe], capture_output=True, text=True).stdout.splitlines()
+    defined = {ln.split()[-1] for ln in syms if " T " in ln}
+    undefined = {ln.split()[-1] for ln in syms if " U " in ln}
+    assert "_ZN7leveldb6crc32c6ExtendEjPKcm" in defined  # the reference's own util/crc32c.cc
+    assert "_ZN7leveldb4HashEPKcmj" in defined
+    assert any("SealBlocks" in u for u in undefined)  # from liblsbm_crc32c.so
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "liblsbm_crc32c.so" in ldd and "libamdhip64" in ldd
