@@ -49,6 +49,17 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32
 }
 
+// The lane's part of a byte-table address, and each table's part (OR-ed into
+// the v_perm constant L[t], whose bytes 0 and 2 land at bits 0..7 and
+// 16..23 of the address, the state byte at bits 8..15).
+#ifdef LSBM_LDS16
+__device__ __forceinline__ uint32_t row_lane_base(uint32_t lane) { return (lane & 15u) << 2; }
+constexpr uint32_t kRowTab[4] = {0x00u, 0x40u, 0x80u, 0xC0u};
+#else
+__device__ __forceinline__ uint32_t row_lane_base(uint32_t lane) { return (lane & 31u) << 2; }
+constexpr uint32_t kRowTab[4] = {0x00u, 0x80u, 0x10000u, 0x10080u};
+#endif
+
 // One braid step: A^128(c) ^ w via the replicated byte tables (L[t] = the
 // lane's constant part of the table-t address), i.e. the reference's STEP4
 // (util/crc32c.cc:295-302) for a 128-byte stride, with the next word folded in.
@@ -87,15 +98,44 @@ __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {  // util/crc32c.h:3
   return (r >> 17) | (r << 15);
 }
 
-// A^4(v) from the uniform LDS nibble tables at kNibA4.
-__device__ __forceinline__ uint32_t adv4_lds(const uint32_t* lds, uint32_t v) {
+// M(v) from uniform LDS nibble tables at `tab` (kNibA4, kNibA8, kNibA12:
+// 512-B aligned, so the and-or merges the nibble field with the base).
+template <uint32_t tab>
+__device__ __forceinline__ uint32_t nib_uniform_lds(const uint32_t* lds, uint32_t v) {
   uint32_t t[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) {
     const uint32_t f = q == 0 ? (v << 2) : (v >> (4 * q - 2));  // nibble q -> bits 2..5
-    t[q] = lds_load(lds, ((f & 0x3cu) | kNibA4) + q * 64);
+    t[q] = lds_load(lds, ((f & 0x3cu) | tab) + q * 64);
   }
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// A^4(v): the uniform nibble tables, or (LSBM_LDS16) the lane's copy of the
+// A^4 byte tables, as a row step with no next word.
+__device__ __forceinline__ uint32_t adv4_lds(const uint32_t* lds, uint32_t v) {
+#ifdef LSBM_LDS16
+  const uint32_t lb = row_lane_base(threadIdx.x) | (kByteA4 >> 16) << 16;
+  return row_step(lds, v, 0u, lb | kRowTab[0], lb | kRowTab[1], lb | kRowTab[2], lb | kRowTab[3]);
+#else
+  return nib_uniform_lds<kNibA4>(lds, v);
+#endif
+}
+
+// The in-lane part of a merge: A^12(c0) ^ A^8(c1) ^ A^4(c2) ^ c3, the four
+// braid words of a lane slice brought to its last word.  As a chain of three
+// A^4 steps (three dependent LDS round trips), or (LSBM_MERGE_PAR) as three
+// independent lookups in one round trip (the same VALU, the same loads).
+__device__ __forceinline__ uint32_t lane_slice(const uint32_t* lds, uint32_t c0, uint32_t c1, uint32_t c2,
+                                               uint32_t c3) {
+#ifdef LSBM_MERGE_PAR
+  return xor3(nib_uniform_lds<kNibA12>(lds, c0), nib_uniform_lds<kNibA8>(lds, c1),
+              xor3(nib_uniform_lds<kNibA4>(lds, c2), c3, 0u));
+#else
+  uint32_t u = adv4_lds(lds, c0) ^ c1;
+  u = adv4_lds(lds, u) ^ c2;
+  return adv4_lds(lds, u) ^ c3;
+#endif
 }
 
 // A^(116-16li)(v) from the lane-replicated LDS tables at kNibFin.
@@ -148,9 +188,7 @@ __device__ __forceinline__ void load_lds_tables(uint32_t* lds, const DevConsts* 
 __device__ __forceinline__ uint32_t merge_braids(const uint32_t* lds, uint32_t c0, uint32_t c1,
                                                  uint32_t c2, uint32_t c3, uint32_t lane_fin) {
   // in-lane: words at 16li + 0, 4, 8, 12 -> one register at 16li + 12
-  uint32_t u = adv4_lds(lds, c0) ^ c1;
-  u = adv4_lds(lds, u) ^ c2;
-  u = adv4_lds(lds, u) ^ c3;
+  uint32_t u = lane_slice(lds, c0, c1, c2, c3);
   // to the end of the row: A^(128 - (16li + 16)) then A^4 = A^(116 - 16li)
   u = fin_lds(lds, u, lane_fin);
   return group_xor(u);
@@ -163,6 +201,11 @@ __device__ __forceinline__ void merge_braids2(const uint32_t* lds, uint32_t a0, 
                                               uint32_t a3, uint32_t b0, uint32_t b1, uint32_t b2,
                                               uint32_t b3, uint32_t lane_fin, uint32_t& xa,
                                               uint32_t& xb) {
+#ifdef LSBM_MERGE_PAR
+  uint32_t u = lane_slice(lds, a0, a1, a2, a3), v = lane_slice(lds, b0, b1, b2, b3);
+  u = fin_lds(lds, u, lane_fin);
+  v = fin_lds(lds, v, lane_fin);
+#else
   uint32_t u = adv4_lds(lds, a0), v = adv4_lds(lds, b0);
   u = adv4_lds(lds, u ^ a1);
   v = adv4_lds(lds, v ^ b1);
@@ -170,6 +213,7 @@ __device__ __forceinline__ void merge_braids2(const uint32_t* lds, uint32_t a0, 
   v = adv4_lds(lds, v ^ b2);
   u = fin_lds(lds, u ^ a3, lane_fin);
   v = fin_lds(lds, v ^ b3, lane_fin);
+#endif
   xa = group_xor(u);
   xb = group_xor(v);
 }

@@ -88,13 +88,27 @@ void build_consts(DevConsts* c) {
   for (int li = 0; li < 8; li++) gf2::nibble_tables(gf2::byte_pow(116 - 16 * li), c->fin_nib[li]);
   // LDS image (layout: crc32c_device.h header comment)
   memset(c->lds_image, 0, sizeof(c->lds_image));
+#ifdef LSBM_LDS16
+  {
+    uint32_t a4[1024];
+    gf2::byte_tables(gf2::byte_pow(4), a4);
+    for (uint32_t w = 0; w < 0x10000 / 4; w++) {
+      const uint32_t a = w << 2, t = (a >> 6) & 3u, b = (a >> 8) & 255u;
+      c->lds_image[w] = c->row_byte[t * 256 + b];
+      c->lds_image[kByteA4 / 4 + w] = a4[t * 256 + b];
+    }
+  }
+#else
   for (uint32_t w = 0; w < kLdsByteTabBytes / 4; w++) {
     const uint32_t a = w << 2;
     const uint32_t t = ((a >> 16) << 1) | ((a >> 7) & 1u);
     const uint32_t b = (a >> 8) & 255u;
     c->lds_image[w] = c->row_byte[t * 256 + b];
   }
+#endif
   for (uint32_t w = 0; w < 128; w++) c->lds_image[kNibA4 / 4 + w] = c->pow_nib[2][w];
+  for (uint32_t w = 0; w < 128; w++) c->lds_image[kNibA8 / 4 + w] = c->pow_nib[3][w];
+  gf2::nibble_tables(gf2::byte_pow(12), &c->lds_image[kNibA12 / 4]);
   for (uint32_t w = 0; w < 8 * 16 * 32; w++) {
     const uint32_t q = w >> 9, nib = (w >> 5) & 15u, slot = w & 31u;
     c->lds_image[kNibFin / 4 + w] = c->fin_nib[slot & 7u][q * 16 + nib];

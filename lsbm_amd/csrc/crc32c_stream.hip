@@ -125,8 +125,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   const DevConsts* __restrict__ dc = args.dc;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
-  const uint32_t lb = (lane & 31u) << 2;
-  const uint32_t L0 = lb, L1 = lb | 0x80u, L2 = lb | 0x10000u, L3 = lb | 0x10080u;
+  const uint32_t lb = row_lane_base(lane);
+  const uint32_t L0 = lb | kRowTab[0], L1 = lb | kRowTab[1], L2 = lb | kRowTab[2], L3 = lb | kRowTab[3];
   const uint32_t lane_fin = kNibFin | lb;
   const uint64_t wave = (uint64_t)blockIdx.x * kStreamWavesPerWg +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

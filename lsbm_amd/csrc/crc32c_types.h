@@ -28,7 +28,20 @@ constexpr int kStreamWavesPerWg = kStreamThreads / kWaveLanes;
 constexpr uint32_t kLdsByteTabBytes = 131072;
 // Nibble tables (byte offsets into LDS).  Bases are chosen so that an
 // and-or can merge the nibble field with the base (disjoint bits).
-constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform)
+constexpr uint32_t kNibA4 = 0x20000;     // A^4, 8 x 16 entries (uniform); A^8 and A^12 at
+                                         // +512 and +1024 (LSBM_MERGE_PAR: merges in one round trip)
+constexpr uint32_t kNibA8 = kNibA4 + 512;
+constexpr uint32_t kNibA12 = kNibA4 + 1024;
+// A/B (round 5): LSBM_LDS16 holds the A^128 byte tables
+// at 16 replicas (64 KiB: lanes l and l + 16 of a half-wave share a bank, a
+// 2-way conflict on the row step) and puts byte tables of A^4, laid out the
+// same way, in the freed 64 KiB at 0x10000: a merge's three A^4 steps become
+// row-step lookups (4 v_perm + 4 ds_read + 2 v_bitop3 each) instead of nibble
+// lookups (8 ds_read and ~20 VALU).  Address of (table t, byte b):
+//   b << 8 | t << 6 | (lane & 15) << 2   (+ 0x10000 for A^4)
+#ifdef LSBM_LDS16
+constexpr uint32_t kByteA4 = 0x10000;
+#endif
 constexpr uint32_t kNibFin = 0x20800;    // A^(116-16li), replicated per lane slot:
                                          // entry (q, nib, lane&31) at q*2048 + nib*128 + lane*4
 constexpr uint32_t kRowPowTables = 21;

@@ -11,7 +11,12 @@ resident in HBM before timing.  One JSON line per measurement:
   bloom_block   lsbm_filter_block_may_match_dev, through FilterBlockReader's
                 offset array (one filter block per 1,024 filters)
 
-Algorithmic bytes (what the roofline fraction uses) are stated per line.
+Algorithmic bytes are stated per line.  The build's roofline fraction uses
+them (its counter bytes are >= them); the probes are reported as queries per
+second and 128-B HBM lines fetched per query (calibrated PMC counters,
+profiles/bloom_traffic.json), with no % of HBM: their queries share filter
+lines, so counter bytes fall below the byte model, and they are bound by
+dependent-load latency, not bandwidth.
 cpu_baseline: the reference's own CreateFilter / KeyMayMatch
 (oracle/_ref/libref_bloom.so, built from /root/reference) on every usable
 host core and on one, on a bounded sample, else the oracle's C restatement.
@@ -298,6 +303,23 @@ def main():
             # gfx950, these scattered reads included (tools/fetch_calib.hip:
             # one memory request per 128-B line, profiles/r04/fetch_calib/)
             ln["roofline"]["traffic_calibration"] = "profiles/r04/fetch_calib/summary.json"
+        q = ln.get("queries")
+        if t and q:
+            # Probes: queries per second and the 128-B lines each one fetches
+            # from HBM (calibrated counters).  Queries share filter lines, so
+            # the counters see fewer bytes than the byte model counts: a % of
+            # HBM from algorithmic bytes would overstate these kernels, which
+            # PMC shows bound by dependent-load latency.
+            # A % of HBM is reported only where counter bytes >= algorithmic.
+            secs = ln["ms"] / 1e3
+            ln["lines_128B_per_query"] = round(t / 128 / q, 3)
+            ln["hbm_GBps_by_counters"] = round(t / secs / 1e9, 1)
+            if t < ln["algorithmic_bytes"]:
+                ln["roofline"] = {"bound": "latency (dependent loads: key -> hash -> filter line)",
+                                  "frac": None, "hbm_frac_by_counters": round(t / secs / 1e9 / HBM, 4),
+                                  "traffic": int(t), "traffic_over_algorithmic": round(t / ln["algorithmic_bytes"], 3),
+                                  "algorithmic_GBps_not_a_roofline": ln["GBps"],
+                                  "traffic_calibration": "profiles/r04/fetch_calib/summary.json"}
         if cpu:
             ln["cpu_baseline"] = cpu
         print(json.dumps(ln), flush=True)
