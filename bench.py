@@ -326,8 +326,15 @@ def main():
     if args.dump_samples:  # tests/test_multirank_gpu.py checks these against the oracle
         idx = np.unique(np.concatenate([np.arange(min(n, 64)), np.arange(max(0, n - 64), n),
                                         np.random.default_rng(rank).integers(0, n, 128)]))
+        # (and every CRC of the shard at once: the XOR of all of them against
+        # the oracle's CRC of the XOR of all blocks, by linearity; after timing)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from golden.xorfold import xor_fold_rows
+        xb = xor_fold_rows(data.view(torch.int64).view(n, BLOCK // 8)).cpu().numpy().view(np.uint8)
+        xc = xor_fold_rows(out.view(n, 1)).cpu().numpy().view(np.uint32)
         np.savez(f"{args.dump_samples}.rank{rank}.npz", gidx=lo + idx, seed=SEED, n=n,
-                 crc=out.cpu().numpy().view(np.uint32)[idx], world=world, t_max=t_max)
+                 crc=out.cpu().numpy().view(np.uint32)[idx], world=world, t_max=t_max,
+                 xor_block=xb, xor_crc=xc)
 
     cpu = staged = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -376,6 +376,22 @@ def test_fill_splitmix64_matches_numpy(torch_cuda):
 
 
 # ---------------------------------------------------------------- full-size configs
+from golden.xorfold import xor_fold_rows  # noqa: E402
+
+
+def crc_linearity_holds(oracle, d, crc, L, n):
+    """Every one of the n CRCs checked at once, at full size: for blocks of one
+    length L, Value(b) = raw(b) ^ Value(0^L) with raw linear over GF(2), so the
+    XOR of all n CRCs equals Value(XOR of all n blocks), ^ Value(0^L) when n is
+    even.  One 4-byte compare against the oracle over the XOR-folded block
+    (folded on the device) covers every block of the batch."""
+    import torch
+    xb = xor_fold_rows(d[:n * L].view(torch.int64).view(n, L // 8)).cpu().numpy().view(np.uint8)
+    xc = int(xor_fold_rows(crc[:n].view(torch.int32).view(n, 1)).cpu().numpy().view(np.uint32)[0])
+    want = oracle.value(xb.tobytes()) ^ (oracle.value(bytes(L)) if n % 2 == 0 else 0)
+    return xc == want
+
+
 def _config_fixed(torch, oracle, golden, name, seed, L, n, check_ragged_blocks):
     from lsbm_amd import engine
     d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
@@ -393,7 +409,12 @@ def _config_fixed(torch, oracle, golden, name, seed, L, n, check_ragged_blocks):
     offs = torch.arange(0, (m + 1) * L, L, dtype=torch.int64, device="cuda")
     other = engine.crc32c_batch(d, offs)
     assert torch.equal(other, crc[:m])
-    del d, crc, other, offs
+    del other, offs
+    # all n CRCs at once, against the oracle, by linearity
+    assert crc_linearity_holds(oracle, d, crc, L, n)
+    crc[n // 3] ^= 1  # (and the check sees a single wrong CRC)
+    assert not crc_linearity_holds(oracle, d, crc, L, n)
+    del d, crc
     torch.cuda.empty_cache()
 
 

@@ -51,6 +51,8 @@ def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
         assert g.min() >= rank * 10_000_000 and g.max() < (rank + 1) * 10_000_000
         for i, c in zip(g, z["crc"]):
             assert c == oracle.value(stream_bytes(0x5EED0000, int(i) * 4096, 4096).tobytes()), (f, int(i))
+        # every CRC of the shard at once, by linearity (10M blocks: n even)
+        assert int(z["xor_crc"][0]) == oracle.value(z["xor_block"].tobytes()) ^ oracle.value(bytes(4096)), f
         seen.append((g.min(), g.max()))
     # rank 1's first block is global block 10M: the shards tile the dataset
     assert sorted(seen)[1][0] == 10_000_000

@@ -16,6 +16,7 @@
 //   run:   build/bench_host_layers [tables=1000] [wal_mb=1024]
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <sys/resource.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -34,6 +35,12 @@ namespace {
 
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// this process's CPU time, every thread (the caller, the pool, HIP's own)
+double cpu_s() {
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
 }
 
 uint64_t splitmix(uint64_t& x) {
@@ -127,17 +134,21 @@ int main(int argc, char** argv) {
     // ~15 ms more, in the runtime, outside the layer's copy / wait / results)
     const int reps = 20;
     std::vector<double> ts, tv;
+    double c0 = cpu_s();
     for (int r = 0; r < reps && s.ok(); r++) {
       const double t0 = now();
       s = lsbm::SealBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.types.data(), t.h.size());
       ts.push_back(now() - t0);
     }
+    const double cpu_seal = (cpu_s() - c0) / reps;
     std::vector<uint8_t> ok;
+    c0 = cpu_s();
     for (int r = 0; r < reps && s.ok(); r++) {
       const double t0 = now();
       s = lsbm::VerifyBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.h.size(), &ok);
       tv.push_back(now() - t0);
     }
+    const double cpu_verify = (cpu_s() - c0) / reps;
     auto mean = [](const std::vector<double>& v) {
       double a = 0;
       for (double x : v) a += x;
@@ -150,9 +161,11 @@ int main(int argc, char** argv) {
     const double el_s = median(ts), el_v = median(tv);
     printf("{\"what\": \"one_table_16MiB\", \"blocks\": %zu, \"status\": \"%s\", \"seal_ms\": %.3f, "
            "\"seal_GBps\": %.2f, \"verify_ms\": %.3f, \"verify_GBps\": %.2f, \"seal_mean_ms\": %.3f, "
-           "\"verify_mean_ms\": %.3f, \"sample_bad\": %d}\n",
+           "\"verify_mean_ms\": %.3f, \"seal_cpu_ms_per_call\": %.3f, \"verify_cpu_ms_per_call\": %.3f, "
+           "\"sample_bad\": %d}\n",
            t.h.size(), s.ToString().c_str(), el_s * 1e3, t.img.size() / el_s / 1e9, el_v * 1e3,
-           t.img.size() / el_v / 1e9, mean(ts) * 1e3, mean(tv) * 1e3, check_table(t, 7));
+           t.img.size() / el_v / 1e9, mean(ts) * 1e3, mean(tv) * 1e3, cpu_seal * 1e3, cpu_verify * 1e3,
+           check_table(t, 7));
   }
   // ---- a compaction: ntables x 16 MiB, pageable and page-locked ----
   {
@@ -174,22 +187,24 @@ int main(int argc, char** argv) {
           }
       // warm at the timed size: the session's stages grow to 64 MiB chunks once
       lsbm::Status s = lsbm::SealTables(0, im.data(), ntables);
-      double t0 = now();
+      double t0 = now(), c0 = cpu_s();
       s = lsbm::SealTables(0, im.data(), ntables);
-      const double el_s = now() - t0;
+      const double el_s = now() - t0, cpu_seal = cpu_s() - c0;
       int bad = 0;
       for (size_t i = 0; i < ntables; i += 37) bad += check_table(ts[i], 13);
       std::vector<uint8_t> ok;
       t0 = now();
+      c0 = cpu_s();
       lsbm::Status v = lsbm::VerifyTables(0, im.data(), ntables, &ok);
-      const double el_v = now() - t0;
+      const double el_v = now() - t0, cpu_verify = cpu_s() - c0;
       size_t nok = 0;
       for (uint8_t o : ok) nok += o;
       printf("{\"what\": \"compaction_tables\", \"tables\": %zu, \"bytes\": %zu, \"pinned\": %d, "
              "\"seal\": \"%s\", \"seal_s\": %.3f, \"seal_GBps\": %.2f, \"verify\": \"%s\", \"verify_s\": %.3f, "
-             "\"verify_GBps\": %.2f, \"blocks_ok\": %zu, \"blocks\": %zu, \"sample_bad\": %d}\n",
+             "\"verify_GBps\": %.2f, \"seal_cpu_ms_per_table\": %.3f, \"verify_cpu_ms_per_table\": %.3f, "
+             "\"blocks_ok\": %zu, \"blocks\": %zu, \"sample_bad\": %d}\n",
              ntables, bytes, pinned, s.ToString().c_str(), el_s, bytes / el_s / 1e9, v.ToString().c_str(),
-             el_v, bytes / el_v / 1e9, nok, ok.size(), bad);
+             el_v, bytes / el_v / 1e9, cpu_seal * 1e3 / ntables, cpu_verify * 1e3 / ntables, nok, ok.size(), bad);
       if (pinned)
         for (auto& t : ts) (void)hipHostUnregister(t.img.data());
     }
@@ -215,18 +230,19 @@ int main(int argc, char** argv) {
       }
     }
     lsbm::Status s = warm.Seal(0);
-    double t0 = now();
+    double t0 = now(), c0 = cpu_s();
     if (s.ok()) s = w.Seal(0);
-    const double el_s = now() - t0;
+    const double el_s = now() - t0, cpu_seal = cpu_s() - c0;
     const std::string& img = w.contents();
     struct Count : lsbm::log::Reporter {
       size_t drops = 0;
       void Corruption(size_t, const lsbm::Status&) override { drops++; }
     } rep;
     t0 = now();
+    c0 = cpu_s();
     lsbm::log::BatchReader r(img.data(), img.size(), &rep);
     lsbm::Status v = r.Verify(0);
-    const double el_v = now() - t0;
+    const double el_v = now() - t0, cpu_verify = cpu_s() - c0;
     std::string rec;
     size_t got = 0;
     t0 = now();
@@ -234,9 +250,11 @@ int main(int argc, char** argv) {
     const double el_r = now() - t0;
     printf("{\"what\": \"wal\", \"bytes\": %zu, \"records\": %zu, \"physical\": %zu, \"seal\": \"%s\", "
            "\"seal_s\": %.3f, \"seal_GBps\": %.2f, \"verify\": \"%s\", \"verify_s\": %.3f, \"verify_GBps\": %.2f, "
-           "\"replay_s\": %.3f, \"records_read\": %zu, \"drops\": %zu}\n",
+           "\"replay_s\": %.3f, \"seal_cpu_ms_per_GB\": %.2f, \"verify_cpu_ms_per_GB\": %.2f, "
+           "\"records_read\": %zu, \"drops\": %zu}\n",
            img.size(), nrec, w.headers().size(), s.ToString().c_str(), el_s, img.size() / el_s / 1e9,
-           v.ToString().c_str(), el_v, img.size() / el_v / 1e9, el_r, got, rep.drops);
+           v.ToString().c_str(), el_v, img.size() / el_v / 1e9, el_r, cpu_seal * 1e3 / (img.size() / 1e9),
+           cpu_verify * 1e3 / (img.size() / 1e9), got, rep.drops);
   }
   return lsbm_crc32c_shutdown() == LSBM_OK ? 0 : 1;
 }
