@@ -137,6 +137,8 @@ class GpuTableBuilder {
   uint64_t FileSize() const { return image_.size(); }  // (reserved trailers included, as the reference's offset)
   size_t SealCalls() const { return seal_calls_; }
   size_t Blocks() const { return handles_.size(); }
+  // every block placed so far: data blocks, then filter, metaindex, index
+  const std::vector<lsbm::BlockHandle>& Handles() const { return handles_; }
 
  private:
   void AddIndexEntry() {

@@ -18,6 +18,13 @@
 //     entry reads back through ReadBlock with verify_checksums on;
 //   * exactly one seal call per table, page-locked in place (one per-call
 //     lock per table: lsbm_test_locks_taken).
+// Then the read side, per table (integration/gpu_table_reader.h): the
+// reference's Table::Open + iteration with verify_checksums (ReadBlock's CRC
+// on every data block, as a paranoid compaction reads its inputs) against
+// OpenVerifiedTable (the whole file read once, ONE VerifyBlocks call over its
+// data blocks, iteration from memory without per-block CRCs): the same
+// entries; a flipped data-block byte gives both the same status; a flipped
+// filter-block byte neither (the reference never checks it either).
 // Configs: 16 MiB tables with a 10-bit bloom filter; lsbm's default 8 MiB
 // (config::kTargetFileSize, common/params.cc:20) with no filter; 16 KiB blocks
 // with kSnappyCompression requested; a 37-entry table; an empty table.
@@ -33,6 +40,7 @@
 
 #include "common/dbformat.h"
 #include "integration/gpu_table_builder.h"
+#include "integration/gpu_table_reader.h"
 #include "leveldb/env.h"
 #include "leveldb/filter_policy.h"
 #include "leveldb/iterator.h"
@@ -134,7 +142,7 @@ int main(int argc, char** argv) {
   };
   const InternalKeyComparator icmp(BytewiseComparator());
   size_t total_tables = 0, total_blocks = 0;
-  double t_ref = 0, t_gpu = 0;
+  double t_ref = 0, t_gpu = 0, t_ref_read = 0, t_gpu_read = 0;
   uint64_t total_bytes = 0;
   for (const Config& c : configs) {
     const FilterPolicy* bloom = c.bloom_bits ? NewBloomFilterPolicy(c.bloom_bits) : nullptr;
@@ -211,9 +219,80 @@ int main(int argc, char** argv) {
         delete it;
         delete table;
       }
+      // ---- read side: the reference's verified iteration vs one GPU verify per table ----
+      const size_t meta_blocks = (ifp ? 1 : 0) + 2;  // filter, metaindex, index
+      const size_t n_data = gpu.Blocks() - meta_blocks;
+      auto ref_read = [&](const std::string& file, size_t* n, bool* match, Status* st) {
+        StringSource rsrc(file);  // (pread-like: every Read copies into ReadBlock's buffer)
+        Table* rt = nullptr;
+        *st = Table::Open(opt, 2000 + t, &rsrc, file.size(), &rt);
+        *n = 0;
+        *match = true;
+        if (!st->ok()) return;
+        ReadOptions ro;
+        ro.verify_checksums = true;  // (a paranoid compaction's input iterator, lsbm/version_set.cc:2311)
+        Iterator* it = rt->NewIterator(ro);
+        for (it->SeekToFirst(); it->Valid(); it->Next(), (*n)++)
+          *match = *match && *n < used && it->key() == Slice(keys[*n]) && it->value() == Slice(vals[*n]);
+        *st = it->status();
+        delete it;
+        delete rt;
+      };
+      auto gpu_read = [&](const std::string& file, size_t* n, bool* match, Status* st, size_t* nblk) {
+        StringSource gsrc(file);
+        std::string image;
+        TableImageFile* imf = nullptr;
+        Table* gt = nullptr;
+        *n = 0;
+        *match = true;
+        *st = OpenVerifiedTable(opt, 3000 + t, &gsrc, file.size(), 0, &image, &imf, &gt, nblk);
+        if (!st->ok()) return;
+        Iterator* it = gt->NewIterator(ReadOptions());  // (verified above: no per-block CRC)
+        for (it->SeekToFirst(); it->Valid(); it->Next(), (*n)++)
+          *match = *match && *n < used && it->key() == Slice(keys[*n]) && it->value() == Slice(vals[*n]);
+        *st = it->status();
+        delete it;
+        delete gt;
+        delete imf;
+      };
+      size_t rn = 0, gn = 0, nblk = 0;
+      bool rmatch = false, gmatch = false;
+      Status rst, gst;
+      const double r0 = now();
+      ref_read(ref_file.data, &rn, &rmatch, &rst);
+      const double r1 = now();
+      gpu_read(ref_file.data, &gn, &gmatch, &gst, &nblk);
+      const double r2 = now();
+      t_ref_read += r1 - r0;
+      t_gpu_read += r2 - r1;
+      EXPECT(rst.ok() && rmatch && rn == used);
+      EXPECT(gst.ok() && gmatch && gn == used);
+      EXPECT(nblk == n_data);
+      if (n_data > 1) {
+        // a flipped byte in a data block: both report ReadBlock's corruption
+        std::string bad = ref_file.data;
+        const lsbm::BlockHandle& hb = gpu.Handles()[n_data / 2];
+        bad[hb.offset + hb.size / 2] ^= 0x08;
+        ref_read(bad, &rn, &rmatch, &rst);
+        gpu_read(bad, &gn, &gmatch, &gst, &nblk);
+        EXPECT(rst.IsCorruption() && gst.IsCorruption());
+        EXPECT(rst.ToString() == gst.ToString());
+        EXPECT(gst.ToString() == "Corruption: block checksum mismatch");
+      }
+      if (ifp && used > 0) {
+        // a flipped byte in the filter block: neither checks it (the reference
+        // reads filters without verify_checksums, table/table.cc:138-144)
+        std::string fb = ref_file.data;
+        const lsbm::BlockHandle& hf = gpu.Handles()[n_data];
+        if (hf.size > 0) fb[hf.offset] ^= 0x01;
+        ref_read(fb, &rn, &rmatch, &rst);
+        gpu_read(fb, &gn, &gmatch, &gst, &nblk);
+        EXPECT(rst.ok() && gst.ok() && rn == used && gn == used);
+      }
       printf("%s table %d: %zu entries, %zu blocks, %zu bytes, identical=%d, reference builder %.1f ms, gpu-sealed "
-             "builder %.1f ms\n",
-             c.name, t, used, gpu.Blocks(), gpu_file.data.size(), (int)same, (t1 - t0) * 1e3, (t2 - t1) * 1e3);
+             "builder %.1f ms; verified read: reference %.1f ms, gpu %.1f ms\n",
+             c.name, t, used, gpu.Blocks(), gpu_file.data.size(), (int)same, (t1 - t0) * 1e3, (t2 - t1) * 1e3,
+             (r1 - r0) * 1e3, (r2 - r1) * 1e3);
       total_tables++;
       total_blocks += gpu.Blocks();
       total_bytes += gpu_file.data.size();
@@ -222,8 +301,10 @@ int main(int argc, char** argv) {
     delete bloom;
   }
   EXPECT(lsbm_test_locked_ranges() == 0);
-  printf("%s tables=%zu blocks=%zu bytes=%llu ref_builder_s=%.3f gpu_builder_s=%.3f\n", fails ? "FAILED" : "OK",
-         total_tables, total_blocks, (unsigned long long)total_bytes, t_ref, t_gpu);
+  printf("%s tables=%zu blocks=%zu bytes=%llu ref_builder_s=%.3f gpu_builder_s=%.3f ref_verified_read_s=%.3f "
+         "gpu_verified_read_s=%.3f\n",
+         fails ? "FAILED" : "OK", total_tables, total_blocks, (unsigned long long)total_bytes, t_ref, t_gpu,
+         t_ref_read, t_gpu_read);
   (void)lsbm_crc32c_shutdown();
   return fails ? 1 : 0;
 }

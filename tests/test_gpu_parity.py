@@ -556,7 +556,12 @@ def test_gpu_sealed_table_builder_matches_the_reference_table_builder(torch_cuda
     and the file is byte-identical to the unmodified TableBuilder's (whose
     trailers come from the reference's own util/crc32c.cc, block by block); the
     reference's Table::Open / ReadBlock with verify_checksums reads every entry
-    back.  Skipped where the binary was not built."""
+    back.  Then the read side (integration/gpu_table_reader.h): the reference's
+    Table::Open + iteration with verify_checksums against OpenVerifiedTable
+    (the file read once, ONE VerifyBlocks call over its data blocks, iteration
+    from memory): the same entries, the same status for a flipped data-block
+    byte, and neither checks the filter block.  Skipped where the binary was
+    not built."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
