@@ -186,6 +186,30 @@ def cpu_baseline(host, gpu_crcs, cpu_seconds):
         el1 = time.perf_counter() - t1
         if el1 >= 3.0:
             break
+    # the strongest CPU CRC-32C the host has (SSE4.2 crc32, three blocks
+    # interleaved), labelled "not reference" (SURVEY.md 8d): lsbm never uses it
+    sse = None
+    sse_path = os.path.join(REPO, "oracle", "libsse42_baseline.so")
+    if not os.path.exists(sse_path):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "libsse42_baseline.so"],
+                       stdout=subprocess.DEVNULL)
+    if os.path.exists(sse_path):
+        hw = ctypes.CDLL(sse_path).sse42_batch_fixed_mt
+        hw.restype = ctypes.c_int
+        hw.argtypes = f.argtypes
+        hw(host.ctypes.data, BLOCK, BLOCK, n, out.ctypes.data, threads)
+        sse_bad = int(np.count_nonzero(out != gpu_crcs[:n]))
+        ps, ts = 0, time.perf_counter()
+        while True:  # >= 2 passes, <= ~3 s
+            hw(host.ctypes.data, BLOCK, BLOCK, n, out.ctypes.data, threads)
+            ps += 1
+            els = time.perf_counter() - ts
+            if ps >= 2 and els >= 1.0 or els > 3.0:
+                break
+        sse = {"value": round(ps * n * BLOCK / 2**30 / els, 3), "unit": "GiB/s", "cores": threads,
+               "kind": "not reference (SSE4.2 crc32, 3 blocks interleaved; oracle/sse42_baseline.c)",
+               "sample": f"{ps} passes x {n} x {BLOCK} B blocks, {els:.1f} s",
+               "gpu_mismatches_on_sample": sse_bad}
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -201,7 +225,8 @@ def cpu_baseline(host, gpu_crcs, cpu_seconds):
                       f"{el:.1f} s wall; {cpu_model}",
             "single_thread": {"value": round(p1 * 8192 * BLOCK / 2**30 / el1, 3), "unit": "GiB/s",
                               "cores": 1, "sample": f"{p1} passes x 8192 blocks, {el1:.1f} s"},
-            "gpu_mismatches_on_sample": mismatches}
+            "gpu_mismatches_on_sample": mismatches,
+            "sse42_not_reference": sse}
 
 
 def host_staged(engine, data, gpu_crcs, n_blocks, reps=3):

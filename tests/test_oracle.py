@@ -76,3 +76,26 @@ def test_oracle_batch_drivers(oracle):
         assert got[i] == oracle.mask(v)
     fx = oracle.batch_fixed(data, 100, 64, 20)
     assert all(fx[i] == oracle.value(data[i * 100:i * 100 + 64].tobytes()) for i in range(20))
+
+
+def test_sse42_cpu_baseline_matches_the_oracle():
+    """bench.py's "not reference" CPU line (oracle/sse42_baseline.c: the x86
+    crc32 instruction, three blocks interleaved) computes crc32c::Value
+    exactly, for block lengths with and without a word tail and any thread
+    count."""
+    import ctypes
+    import os
+    import subprocess
+    import numpy as np
+    from conftest import Oracle
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(repo, "oracle")], check=True)
+    o = Oracle(os.path.join(repo, "oracle", "liboracle_crc32c.so"))
+    f = ctypes.CDLL(os.path.join(repo, "oracle", "libsse42_baseline.so")).sse42_batch_fixed_mt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                  ctypes.c_int]
+    for blen, stride, n, threads in ((4096, 4096, 1001, 3), (4118, 4123, 77, 2), (13, 16, 10, 1), (0, 8, 4, 2)):
+        d = np.random.default_rng(blen).integers(0, 256, max(1, n * stride), dtype=np.uint8)
+        out = np.empty(n, np.uint32)
+        assert f(d.ctypes.data, stride, blen, n, out.ctypes.data, threads) == 0
+        assert np.array_equal(out, o.batch_fixed(d, stride, blen, n)), (blen, stride)
