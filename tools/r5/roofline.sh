@@ -20,6 +20,7 @@ for e in $ENTRIES; do
     python3 tools/roofline_all.py $e --reps 5 > $OUT/$e/pmc.log 2>&1
   rc=$?; echo "$e pmc rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/$e/pmc.log; exit $rc; }
   python3 tools/r5/roofline_summary.py $OUT $e || exit 1
-  rm -f $OUT/$e/pmc/run_counter_collection.csv $OUT/$e/stats/run_kernel_trace.csv
+  rm -f $OUT/$e/pmc/run_counter_collection.csv
+  [ -n "$KEEP_TRACE" ] || rm -f $OUT/$e/stats/run_kernel_trace.csv
 done
 python3 tools/r5/roofline_summary.py $OUT
