@@ -575,6 +575,31 @@ def test_gpu_sealed_table_builder_matches_the_reference_table_builder(torch_cuda
     assert r.stdout.count("identical=1") == 3 + 3 + 3 + 1 + 1
 
 
+def test_compaction_end_to_end_with_both_gpu_ends_matches_the_reference(torch_cuda):
+    """One compaction as DoCompactionWork runs it with paranoid_checks
+    (tests/cpp/ref_compaction_gpu.cc, oracle/Makefile gpucompact): 4 overlapping
+    16 MiB input tables merged by the reference's MergingIterator into 16 MiB
+    output tables.  The reference's way (verified input iterators, TableBuilder)
+    and with the two GPU ends (OpenVerifiedTable inputs: one VerifyBlocks per
+    input; GpuTableBuilder outputs: one SealBlocks per output) write
+    byte-identical output tables, three rounds.  Skipped where the binary was
+    not built."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                       "gpu_compaction")
+    if not os.access(exe, os.X_OK):
+        pytest.skip("oracle/_ref/gpu_compaction not built (needs /root/reference at build time)")
+    r = subprocess.run([exe, "4", "16", "16"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    last = r.stdout.strip().splitlines()[-1]
+    assert last.startswith("OK") and "FAIL" not in r.stdout, r.stdout
+    f = dict(kv.split("=") for kv in last.split()[1:])
+    assert int(f["outputs"]) >= 4 and f["identical"] == f["outputs"]
+    assert int(f["input_blocks_verified"]) > 16000
+
+
 def test_cpp_block_compression_layer(torch_cuda, tmp_path):
     """include/lsbm/block_compression.h from C++: WriteBlock's compression and
     12.5% rule against the snappy oracle, ReadBlock's decompression and its

@@ -68,7 +68,8 @@ def test_gpu_table_builder_compiles_and_links_against_the_reference():
     gputable): the unmodified TableBuilder in the binary takes Extend and Hash
     from the reference's sources, the GPU builder SealBlocks from the library.
     tests/test_gpu_parity.py runs it on the GPU."""
-    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "gputable"], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "gputable", "gpucompact"], check=True)
+    assert os.access(os.path.join(REPO, "oracle", "_ref", "gpu_compaction"), os.X_OK)
     exe = os.path.join(REPO, "oracle", "_ref", "gpu_table_builder")
     assert os.access(exe, os.X_OK)
     syms = subprocess.run(["nm", exe], capture_output=True, text=True).stdout.splitlines()
