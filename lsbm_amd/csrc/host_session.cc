@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -82,10 +83,17 @@ std::mutex g_lock_mu;
 std::map<uintptr_t, uintptr_t> g_locked;  // [first page, end page) of each live CallLocks range
 std::atomic<long> g_locks_taken{0};        // (testing: ranges locked since start-up)
 
-constexpr uintptr_t kPage = 4096;
-uintptr_t page_lo(const void* p) { return reinterpret_cast<uintptr_t>(p) & ~(kPage - 1); }
+// (the granularity of a registration: the system page)
+uintptr_t page_size() {
+  static const uintptr_t ps = [] {
+    const long v = sysconf(_SC_PAGESIZE);
+    return v > 0 ? (uintptr_t)v : (uintptr_t)4096;
+  }();
+  return ps;
+}
+uintptr_t page_lo(const void* p) { return reinterpret_cast<uintptr_t>(p) & ~(page_size() - 1); }
 uintptr_t page_hi(const void* p, size_t n) {
-  return (reinterpret_cast<uintptr_t>(p) + n + kPage - 1) & ~(kPage - 1);
+  return (reinterpret_cast<uintptr_t>(p) + n + page_size() - 1) & ~(page_size() - 1);
 }
 // (under g_lock_mu)
 bool touches_locked(uintptr_t lo, uintptr_t hi) {
