@@ -329,6 +329,18 @@ def main():
                         mark_start=lambda: ev0.record(stream), mark_end=lambda: ev1.record(stream))
     kern_ms = ev0.elapsed_time(ev1)  # the K launches, HIP events on the launch stream
 
+    # per-launch HIP events after the timed region (SURVEY.md 8d asks for the
+    # median launch): each launch bracketed by its own pair of events
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(3, args.steps))]
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    per_launch_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    median_ms = per_launch_ms[len(per_launch_ms) // 2]
+
     # stream-read ceiling on the same buffer (same stream, same events)
     sink = torch.zeros(1024, dtype=torch.int32, device="cuda")
     for _ in range(3):
@@ -396,7 +408,9 @@ def main():
                          "traffic": traffic,
                          "kernel": "crc32c_fixed_kernel<false,32>",
                          "algorithmic_bytes_per_launch": n * BLOCK,
-                         "avg_launch_ms": round(per_launch_s * 1e3, 4)},
+                         "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                         "median_launch_ms": round(median_ms, 4),
+                         "frac_at_median": round(n * BLOCK / (median_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "stream_read": {"GBps": round(stream_gbps, 1),
                             "crc_frac_of_stream_read": round(achieved / stream_gbps, 4)},
             "cpu_baseline": cpu,
