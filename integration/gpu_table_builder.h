@@ -53,7 +53,10 @@ namespace leveldb {
 class GpuTableBuilder {
  public:
   // Builds a table for `file` (not closed here), sealing on HIP `device`.
-  GpuTableBuilder(const Options& options, WritableFile* file, int device = 0)
+  // size_hint: the table size the caller expects (a compaction knows its
+  // MaxOutputFileSize): the image is reserved once instead of growing by
+  // reallocation, each of which copies everything so far.
+  GpuTableBuilder(const Options& options, WritableFile* file, int device = 0, uint64_t size_hint = 0)
       : options_(options),
         index_options_(options),
         file_(file),
@@ -63,6 +66,7 @@ class GpuTableBuilder {
         filter_(options.filter_policy ? new FilterBlockBuilder(options.filter_policy) : nullptr) {
     index_options_.block_restart_interval = 1;  // (every index entry a restart point)
     if (filter_) filter_->StartBlock(0);
+    if (size_hint) image_.reserve(size_hint + size_hint / 8 + (64u << 10));  // (+ meta blocks, the last block)
   }
   ~GpuTableBuilder() { delete filter_; }
 

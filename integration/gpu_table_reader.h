@@ -10,7 +10,7 @@
 // reads each input table whole, front to back.
 //
 // What this does instead (OpenVerifiedTable): one read of the whole file into
-// a heap image, the index block parsed with the reference's own ReadBlock and
+// a heap image (owned by the TableImageFile the table reads from), the index block parsed with the reference's own ReadBlock and
 // Block (no checksum, as Table::Open reads it, table/table.cc:67-76), ONE
 // VerifyBlocks call over all data blocks -- the image is writable heap memory,
 // so it is page-locked for the call and DMA-ed in place (~0.35 ms per 16 MiB
@@ -45,53 +45,59 @@
 
 namespace leveldb {
 
-// A table image held in memory as a RandomAccessFile: reads return pointers
-// into the image (ReadBlock then uses them in place, table/format.cc:105-112).
+// A table image held in memory as a RandomAccessFile, owning the image:
+// reads return pointers into it (ReadBlock then uses them in place,
+// table/format.cc:105-112).  The buffer is `new char[]` (no zero fill: the
+// file's bytes are read straight into it), writable heap memory, so
+// VerifyBlocks page-locks it for its call.
 class TableImageFile : public RandomAccessFile {
  public:
-  explicit TableImageFile(const std::string* image) : image_(image) {}
+  explicit TableImageFile(uint64_t size) : data_(new char[size ? size : 1]), size_(size) {}
+  ~TableImageFile() { delete[] data_; }
   Status Read(uint64_t offset, size_t n, Slice* result, char*) const {
-    if (offset > image_->size()) return Status::IOError("table image", "read past the end");
-    *result = Slice(image_->data() + offset, std::min<uint64_t>(n, image_->size() - offset));
+    if (offset > size_) return Status::IOError("table image", "read past the end");
+    *result = Slice(data_ + offset, std::min<uint64_t>(n, size_ - offset));
     return Status::OK();
   }
+  char* data() { return data_; }
+  uint64_t size() const { return size_; }
 
  private:
-  const std::string* image_;
+  char* data_;
+  uint64_t size_;
+  TableImageFile(const TableImageFile&);
+  void operator=(const TableImageFile&);
 };
 
-// Reads `file` (size bytes) whole into *image, verifies every data block on
-// HIP device `device` in one call, and on success opens *table over
-// *image_file (both owned by the caller; the table must be deleted before
-// them).  *data_blocks receives the number of blocks verified.
+// Reads `file` (size bytes) whole into a new *image_file, verifies every data
+// block on HIP device `device` in one call, and on success opens *table over
+// it (the caller deletes the table, then the image file).  *data_blocks
+// receives the number of blocks verified.
 inline Status OpenVerifiedTable(const Options& options, uint64_t file_number, RandomAccessFile* file,
-                                uint64_t size, int device, std::string* image, TableImageFile** image_file,
-                                Table** table, size_t* data_blocks) {
+                                uint64_t size, int device, TableImageFile** image_file, Table** table,
+                                size_t* data_blocks) {
   *table = nullptr;
   *image_file = nullptr;
   *data_blocks = 0;
   if (size < Footer::kEncodedLength) return Status::InvalidArgument("file is too short to be an sstable");
-  image->resize(size);
+  TableImageFile* f = new TableImageFile(size);
   Slice got;
-  Status s = file->Read(0, size, &got, &(*image)[0]);
-  if (!s.ok()) return s;
-  if (got.size() != size) return Status::Corruption("truncated block read");
-  if (got.data() != image->data()) memcpy(&(*image)[0], got.data(), size);  // (a file that hands out its own memory)
-  Slice tail(image->data() + size - Footer::kEncodedLength, Footer::kEncodedLength);
-  Footer footer;
-  s = footer.DecodeFrom(&tail);
-  if (!s.ok()) return s;
-
-  // the data blocks, from the index block (read as Table::Open reads it)
-  TableImageFile* f = new TableImageFile(image);
-  BlockContents index_contents;
-  s = ReadBlock(f, ReadOptions(), footer.index_handle(), &index_contents);
+  Status s = file->Read(0, size, &got, f->data());
+  if (s.ok() && got.size() != size) s = Status::Corruption("truncated block read");
   if (!s.ok()) {
     delete f;
     return s;
   }
+  if (got.data() != f->data()) memcpy(f->data(), got.data(), size);  // (a file that hands out its own memory)
+  Slice tail(f->data() + size - Footer::kEncodedLength, Footer::kEncodedLength);
+  Footer footer;
+  s = footer.DecodeFrom(&tail);
+
+  // the data blocks, from the index block (read as Table::Open reads it)
+  BlockContents index_contents;
+  if (s.ok()) s = ReadBlock(f, ReadOptions(), footer.index_handle(), &index_contents);
   std::vector<lsbm::BlockHandle> handles;
-  {
+  if (s.ok()) {
     Block index(index_contents);
     Iterator* it = index.NewIterator(options.comparator);
     for (it->SeekToFirst(); it->Valid() && s.ok(); it->Next()) {
@@ -103,28 +109,24 @@ inline Status OpenVerifiedTable(const Options& options, uint64_t file_number, Ra
     if (s.ok()) s = it->status();
     delete it;
   }
-  if (!s.ok()) {
-    delete f;
-    return s;
-  }
 
   // ONE check of every data block's trailer on the GPU (ReadBlock's
   // verify_checksums test, table/format.cc:95-103, for all of them at once)
-  const lsbm::Status v = lsbm::VerifyBlocks(device, &(*image)[0], image->size(), handles.data(),
-                                            handles.size(), nullptr);
-  if (!v.ok()) {
-    delete f;
-    const std::string m = v.ToString();
-    const std::string kC = "Corruption: ";
-    return v.IsCorruption() ? Status::Corruption(m.substr(m.compare(0, kC.size(), kC) == 0 ? kC.size() : 0))
-                            : Status::IOError("gpu verify", m);
+  if (s.ok()) {
+    const lsbm::Status v = lsbm::VerifyBlocks(device, f->data(), size, handles.data(), handles.size(), nullptr);
+    if (!v.ok()) {
+      const std::string m = v.ToString();
+      const std::string kC = "Corruption: ";
+      s = v.IsCorruption() ? Status::Corruption(m.substr(m.compare(0, kC.size(), kC) == 0 ? kC.size() : 0))
+                           : Status::IOError("gpu verify", m);
+    }
   }
-  *data_blocks = handles.size();
-  s = Table::Open(options, file_number, f, size, table);
+  if (s.ok()) s = Table::Open(options, file_number, f, size, table);
   if (!s.ok()) {
     delete f;
     return s;
   }
+  *data_blocks = handles.size();
   *image_file = f;
   return Status::OK();
 }

@@ -19,10 +19,16 @@
 // compactions run three times; the steady-state time (the best of rounds 2-3)
 // and the first round's are printed.
 //
+// Built twice (oracle/Makefile gpucompact): gpu_compaction's CPU side is the
+// reference's own util/crc32c.cc (slice-by-4); gpu_compaction_l1's
+// (-DLSBM_LEVEL1_CPU) is the same table/ code relinked against the library's
+// scalar Extend (Level 1 of INTEGRATION.md: the x86 crc32 instruction).
+//
 // usage: ref_compaction_gpu [inputs=4] [input_mib=16] [output_mib=16]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 
 #include <chrono>
 #include <string>
@@ -55,6 +61,11 @@ int fails = 0;
 
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double cpu_now() {  // this process's CPU time, every thread
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
 }
 
 class StringSink : public WritableFile {
@@ -89,6 +100,19 @@ uint64_t xs(uint64_t& x) {
   return x;
 }
 
+// A builder for one output table (the GPU builder reserves its image at the
+// compaction's target size, as DoCompactionWork knows MaxOutputFileSize).
+template <class B>
+B* make_builder(const Options& opt, WritableFile* f, uint64_t target);
+template <>
+TableBuilder* make_builder<TableBuilder>(const Options& opt, WritableFile* f, uint64_t) {
+  return new TableBuilder(opt, f);
+}
+template <>
+GpuTableBuilder* make_builder<GpuTableBuilder>(const Options& opt, WritableFile* f, uint64_t target) {
+  return new GpuTableBuilder(opt, f, 0, target);
+}
+
 // Runs the merge of `children` into tables of about `target` bytes, through
 // builder B (TableBuilder or GpuTableBuilder); returns the output files.
 template <class B>
@@ -111,7 +135,7 @@ std::vector<std::string> merge_into_tables(const Options& opt, Iterator** childr
   for (merged->SeekToFirst(); merged->Valid(); merged->Next()) {
     if (!b) {
       sink = new StringSink;
-      b = new B(opt, sink);
+      b = make_builder<B>(opt, sink, target);
     }
     b->Add(merged->key(), merged->value());
     if (b->FileSize() >= target) finish();
@@ -173,10 +197,10 @@ int main(int argc, char** argv) {
   std::vector<std::string> ref_out, gpu_out;
   Status rs, gs;
   size_t verified = 0;
-  double ref_ms[3] = {0, 0, 0}, gpu_ms[3] = {0, 0, 0};
+  double ref_ms[3] = {0, 0, 0}, gpu_ms[3] = {0, 0, 0}, ref_cpu[3] = {0, 0, 0}, gpu_cpu[3] = {0, 0, 0};
   for (int round = 0; round < 3; round++) {
     // ---- the reference: verified input iterators, TableBuilder outputs ----
-    const double t0 = now();
+    const double t0 = now(), c0 = cpu_now();
     std::vector<StringSource*> srcs;
     std::vector<Table*> rtabs;
     std::vector<Iterator*> rits;
@@ -193,13 +217,13 @@ int main(int argc, char** argv) {
     rs = Status::OK();
     ref_out = merge_into_tables<TableBuilder>(opt, rits.data(), K, out_bytes, &rs);
     ref_ms[round] = (now() - t0) * 1e3;
+    ref_cpu[round] = (cpu_now() - c0) * 1e3;
     for (Table* t : rtabs) delete t;
     for (StringSource* s : srcs) delete s;
     srcs.clear();
 
     // ---- the GPU ends: OpenVerifiedTable inputs, GpuTableBuilder outputs ----
-    const double t2 = now();
-    std::vector<std::string> images(K);
+    const double t2 = now(), c2 = cpu_now();
     std::vector<TableImageFile*> imfs(K, nullptr);
     std::vector<Table*> gtabs(K, nullptr);
     std::vector<Iterator*> gits;
@@ -207,8 +231,7 @@ int main(int argc, char** argv) {
     for (int j = 0; j < K; j++) {
       srcs.push_back(new StringSource(inputs[j]));
       size_t nb = 0;
-      EXPECT(OpenVerifiedTable(opt, 20 + j, srcs.back(), inputs[j].size(), 0, &images[j], &imfs[j], &gtabs[j],
-                               &nb).ok());
+      EXPECT(OpenVerifiedTable(opt, 20 + j, srcs.back(), inputs[j].size(), 0, &imfs[j], &gtabs[j], &nb).ok());
       verified += nb;
       ReadOptions fast;  // (verified above)
       fast.fill_cache = false;
@@ -217,6 +240,7 @@ int main(int argc, char** argv) {
     gs = Status::OK();
     gpu_out = merge_into_tables<GpuTableBuilder>(opt, gits.data(), K, out_bytes, &gs);
     gpu_ms[round] = (now() - t2) * 1e3;
+    gpu_cpu[round] = (cpu_now() - c2) * 1e3;
     for (Table* t : gtabs) delete t;
     for (TableImageFile* f : imfs) delete f;
     for (StringSource* s : srcs) delete s;
@@ -234,11 +258,18 @@ int main(int argc, char** argv) {
   uint64_t in_total = 0;
   for (const auto& s : inputs) in_total += s.size();
   const double ref_steady = std::min(ref_ms[1], ref_ms[2]), gpu_steady = std::min(gpu_ms[1], gpu_ms[2]);
-  printf("%s inputs=%d input_bytes=%llu entries=%llu input_blocks_verified=%zu outputs=%zu identical=%zu "
-         "output_bytes=%llu reference_ms=%.1f gpu_ends_ms=%.1f speedup=%.2f first_round_ms=%.1f/%.1f\n",
-         fails ? "FAILED" : "OK", K, (unsigned long long)in_total, (unsigned long long)total_entries, verified,
-         ref_out.size(), identical, (unsigned long long)out_total, ref_steady, gpu_steady, ref_steady / gpu_steady,
-         ref_ms[0], gpu_ms[0]);
+  const double ref_cpu_s = std::min(ref_cpu[1], ref_cpu[2]), gpu_cpu_s = std::min(gpu_cpu[1], gpu_cpu[2]);
+#ifdef LSBM_LEVEL1_CPU
+  const char* cpu_side = "level1_cpu";  // (the table/ code's crc32c::Extend from liblsbm_crc32c.so)
+#else
+  const char* cpu_side = "reference";  // (the reference's own util/crc32c.cc)
+#endif
+  printf("%s cpu_side=%s inputs=%d input_bytes=%llu entries=%llu input_blocks_verified=%zu outputs=%zu identical=%zu "
+         "output_bytes=%llu cpu_ms=%.1f gpu_ends_ms=%.1f speedup=%.2f cpu_side_cpu_ms=%.1f gpu_ends_cpu_ms=%.1f "
+         "first_round_ms=%.1f/%.1f\n",
+         fails ? "FAILED" : "OK", cpu_side, K, (unsigned long long)in_total, (unsigned long long)total_entries,
+         verified, ref_out.size(), identical, (unsigned long long)out_total, ref_steady, gpu_steady,
+         ref_steady / gpu_steady, ref_cpu_s, gpu_cpu_s, ref_ms[0], gpu_ms[0]);
   delete bloom;
   (void)lsbm_crc32c_shutdown();
   return fails ? 1 : 0;

@@ -240,12 +240,11 @@ int main(int argc, char** argv) {
       };
       auto gpu_read = [&](const std::string& file, size_t* n, bool* match, Status* st, size_t* nblk) {
         StringSource gsrc(file);
-        std::string image;
         TableImageFile* imf = nullptr;
         Table* gt = nullptr;
         *n = 0;
         *match = true;
-        *st = OpenVerifiedTable(opt, 3000 + t, &gsrc, file.size(), 0, &image, &imf, &gt, nblk);
+        *st = OpenVerifiedTable(opt, 3000 + t, &gsrc, file.size(), 0, &imf, &gt, nblk);
         if (!st->ok()) return;
         Iterator* it = gt->NewIterator(ReadOptions());  // (verified above: no per-block CRC)
         for (it->SeekToFirst(); it->Valid(); it->Next(), (*n)++)
