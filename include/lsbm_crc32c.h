@@ -239,6 +239,11 @@ int lsbm_test_pool_helpers(int pieces, int piece_us, int max_helpers);
  * page-locked since start-up (which calls DMA-ed an image in place). */
 int lsbm_test_locked_ranges(void);
 long lsbm_test_locks_taken(void);
+/* Testing: the C++ layers' sessions of `device`, and the page-locked staging
+ * bytes they hold (kept near LSBM_PINNED_MB per device by freeing idle
+ * sessions' buffers when a lease is released). */
+int lsbm_test_session_count(int device);
+unsigned long long lsbm_test_pinned_bytes(int device);
 /* Testing: `callers` threads each run `jobs` parallel jobs of 1..max_pieces
  * pieces (some with nested jobs); returns how many pieces did not run exactly
  * once (0 = correct), -1 for bad arguments. */

@@ -62,6 +62,8 @@ SIGNATURES = {
     "lsbm_test_pool_helpers": (_int, [_int, _int, _int]),
     "lsbm_test_locked_ranges": (_int, []),
     "lsbm_test_locks_taken": (ctypes.c_long, []),
+    "lsbm_test_session_count": (_int, [_int]),
+    "lsbm_test_pinned_bytes": (ctypes.c_ulonglong, [_int]),
     "lsbm_test_pool_overlap": (_int, [_int, _int, _int, _int, _vp]),
     "lsbm_test_host_pinned": (_int, [_vp, _sz]),
     "lsbm_test_host_copy": (_int, [_vp, _vp, _sz, _int]),

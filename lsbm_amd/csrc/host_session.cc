@@ -1028,3 +1028,13 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_locked_ranges(vo
 extern "C" __attribute__((visibility("default"))) long lsbm_test_locks_taken(void) {
   return lsbm::locks_taken();
 }
+
+// Testing: the C++ layers' sessions of `device` and the page-locked staging
+// bytes they hold (the pinned budget, LSBM_PINNED_MB).
+extern "C" __attribute__((visibility("default"))) int lsbm_test_session_count(int device) {
+  return lsbm::session_count(device);
+}
+
+extern "C" __attribute__((visibility("default"))) unsigned long long lsbm_test_pinned_bytes(int device) {
+  return (unsigned long long)lsbm::pinned_bytes(device);
+}

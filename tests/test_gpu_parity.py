@@ -528,6 +528,30 @@ def test_cpp_concurrent_callers_on_shared_pages(torch_cuda, oracle, tmp_path, au
         assert int(fields["locked_calls"]) == 0
 
 
+def test_cpp_pinned_staging_stays_within_the_budget(torch_cuda, tmp_path):
+    """a device's sessions (up to 8, 4 stages each) used to keep
+    their page-locked staging until shutdown.  With LSBM_PINNED_MB=8 and every
+    call staged (LSBM_AUTO_LOCK=0), 6 concurrent callers' sessions grow their
+    buffers, and once the leases are released the pinned bytes are back under
+    the budget plus the last session's; later calls grow them again and stay
+    correct; shutdown frees everything (tests/cpp/pinned_budget_test.cc)."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "pinned_budget_test"
+    libdir = os.path.join(repo, "lsbm_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(repo, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(repo, "tests", "cpp", "pinned_budget_test.cc"), "-L", libdir,
+                    "-llsbm_crc32c", "-L", "/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    env = dict(os.environ, LSBM_PINNED_MB="8", LSBM_AUTO_LOCK="0")
+    r = subprocess.run([str(exe), "6"], capture_output=True, text=True, timeout=120, env=env)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "FAIL" not in r.stdout and r.stdout.strip().splitlines()[-1].startswith("OK"), r.stdout
+
+
 def test_level2_binding_over_the_reference_table_code(torch_cuda):
     """integration/leveldb_gpu_checksum.h, linked with the reference's own
     table/ and util/ objects (oracle/Makefile gpubind, built in the build
