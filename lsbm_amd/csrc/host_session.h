@@ -88,6 +88,7 @@ struct Stage {
   // 15-20 us, profiles/r04/one_table_trace/summary_call40.txt).
   bool settled = false;
   uint64_t tag = 0;   // the caller's chunk number
+  double wait_ewma_us = 0;  // moving average of this stage's waits (HostSession::wait)
   StagePair bulk, meta, res;
   StagePair zmeta;  // mapped: per-block inputs the kernel reads in place (zero-copy table jobs)
 };
@@ -128,7 +129,10 @@ class HostSession {
   hipError_t upload(void* d, const void* h, size_t n);
   hipError_t download(void* h, const void* d, size_t n);
 
-  // Waits for a stage's enqueued work (no-op if idle); clears busy.
+  // Waits for a stage's enqueued work (no-op if idle); clears busy.  Sleeps
+  // in short naps while the work is expected to take longer than ~60 us more
+  // (a moving average of the stage's waits), then spins (LSBM_WAIT=spin: spin
+  // throughout).
   hipError_t wait(Stage& s);
 
   // The session's copy stream (created on first use): page-locked chunks'
@@ -268,6 +272,10 @@ struct HostTiming {
 // true once, when a pipeline that has enqueued `enqueued` chunks reaches the
 // armed count.
 bool host_fault_point(size_t enqueued);
+
+// Stage waits sleep on blocking-sync events instead of spinning
+// (LSBM_BLOCKING_WAIT=1).
+bool blocking_wait();
 
 // Status for a failed HIP call.
 Status hip_status(hipError_t e, const char* what);
