@@ -112,6 +112,12 @@ def main():
             data = stream_bytes(seed, b * bsz, bsz).tobytes()
             cfg.append({"config": name, "seed": seed, "block": b, "block_bytes": bsz,
                         "value": ref_extend(0, data)})
+    # config 5 (80M x 4 KiB over 8 shards of 10M, the same stream as config 2):
+    # the blocks either side of every shard boundary, and the last block
+    for b in [10_000_000 * r + d for r in range(1, 8) for d in (-1, 0)] + [79_999_999]:
+        data = stream_bytes(0x5EED0000, b * 4096, 4096).tobytes()
+        cfg.append({"config": "cfg5_shards", "seed": 0x5EED0000, "block": b, "block_bytes": 4096,
+                    "value": ref_extend(0, data)})
     out["config_blocks"] = cfg
 
     path = os.path.join(HERE, "crc32c_golden.json")

@@ -426,6 +426,41 @@ def test_config3_full_1M_x_64KiB(torch_cuda, oracle, golden):
     _config_fixed(torch_cuda, oracle, golden, "cfg3_64k", 0x5EED0001, 65536, 1 << 20, 1 << 16)
 
 
+def test_config5_all_eight_shards(torch_cuda, oracle, golden):
+    """Config 5 (BASELINE.json configs[4]): 80M x 4 KiB over 8 ranks, rank r
+    holding global blocks [10M r, 10M (r + 1)).  The 8-GPU bench is the
+    driver's, so here every shard runs in turn on the one GPU through bench.py's
+    own shard code (the fill from word 512 lo, lsbm_crc32c_fixed_dev over 10M
+    blocks): the reference's CRCs either side of every shard boundary
+    (golden cfg5_shards, from the reference's Extend), 64 sampled blocks per
+    shard against the oracle by global index, and all 10M CRCs of every shard
+    by linearity -- every one of the 80M CRCs is covered."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    n, L, seed = 10_000_000, 4096, 0x5EED0000
+    want = {g["block"]: g["value"] for g in golden["config_blocks"] if g["config"] == "cfg5_shards"}
+    assert len(want) == 15
+    d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    crc = torch.empty(n, dtype=torch.int32, device="cuda")
+    rng = np.random.default_rng(5)
+    seen = 0
+    for r in range(8):
+        lo = r * n
+        engine.fill_splitmix64(d, seed + lo * (L // 8))  # (bench.py main: the same expression)
+        engine.crc32c_fixed(d, L, L, n, out=crc)
+        got = _u32(crc)
+        for b, v in want.items():
+            if lo <= b < lo + n:
+                assert got[b - lo] == v, (r, b)
+                seen += 1
+        for i in rng.choice(n, size=64, replace=False):
+            assert got[i] == oracle.value(stream_bytes(seed, (lo + int(i)) * L, L).tobytes()), (r, int(i))
+        assert crc_linearity_holds(oracle, d, crc, L, n), r
+    assert seen == 15
+    del d, crc
+    torch.cuda.empty_cache()
+
+
 # ---------------------------------------------------------------- C++ host layer
 @pytest.mark.parametrize("small,auto_lock", [("", "1"), ("", "0"), ("zc", "1")],
                          ids=["small-dma-auto-lock", "staged", "small-zero-copy"])
