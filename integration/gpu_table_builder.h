@@ -86,10 +86,32 @@ class GpuTableBuilder {
     if (data_.CurrentSizeEstimate() >= options_.block_size) Flush();
   }
 
+  // TableBuilder::ChangeOptions (table/table_builder.cc:92-106): the
+  // comparator may not change; the block builders see the new options.
+  Status ChangeOptions(const Options& options) {
+    if (options.comparator != options_.comparator)
+      return Status::InvalidArgument("changing comparator while building table");
+    options_ = options;
+    index_options_ = options;
+    index_options_.block_restart_interval = 1;
+    return Status::OK();
+  }
+
+  // An observer of each data block as it is placed (its contents as stored,
+  // i.e. after compression), for what the reference does beside the write:
+  // lsbm's pre-caching (table/table_builder.cc:195-230).  `closing` is true
+  // for the block Finish closes, which the reference never caches (it calls
+  // Flush(false), :263).
+  typedef void (*DataBlockObserver)(void* arg, const Slice& contents, bool closing);
+  void SetDataBlockObserver(DataBlockObserver fn, void* arg) {
+    observer_ = fn;
+    observer_arg_ = arg;
+  }
+
   // Closes the current data block (its trailer reserved, not computed).
   void Flush() {
     if (closed_ || !status_.ok() || data_.empty()) return;
-    PlaceBlock(&data_, &due_handle_);
+    PlaceBlock(&data_, &due_handle_, true);
     index_due_ = true;
     if (filter_) filter_->StartBlock(image_.size());
   }
@@ -97,6 +119,7 @@ class GpuTableBuilder {
   // The meta blocks, ONE seal of every trailer on the GPU, the footer, and
   // the whole image into the file.
   Status Finish() {
+    closing_ = true;
     Flush();
     closed_ = true;
     BlockHandle filter_at, meta_at, index_at;
@@ -154,7 +177,7 @@ class GpuTableBuilder {
 
   // A built block: compressed when the options ask for it and snappy saves
   // at least 1/8 (table/table_builder.cc:176-193), else raw.
-  void PlaceBlock(BlockBuilder* b, BlockHandle* at) {
+  void PlaceBlock(BlockBuilder* b, BlockHandle* at, bool data_block = false) {
     const Slice raw = b->Finish();
     Slice contents = raw;
     CompressionType type = kNoCompression;
@@ -163,6 +186,7 @@ class GpuTableBuilder {
       contents = packed_;
       type = kSnappyCompression;
     }
+    if (data_block && observer_) observer_(observer_arg_, contents, closing_);
     Place(contents, type, at);
     packed_.clear();
     b->Reset();
@@ -196,6 +220,9 @@ class GpuTableBuilder {
   std::vector<lsbm::BlockHandle> handles_;  // every block of the image, for the seal
   std::vector<uint8_t> types_;
   size_t seal_calls_ = 0;
+  bool closing_ = false;  // inside Finish
+  DataBlockObserver observer_ = nullptr;
+  void* observer_arg_ = nullptr;
 
   GpuTableBuilder(const GpuTableBuilder&);
   void operator=(const GpuTableBuilder&);

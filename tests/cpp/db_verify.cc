@@ -1,0 +1,221 @@
+// tests/cpp/db_verify.cc -- the checker of test_db_bench_gpu_tables: a lsbm
+// database directory examined with the REFERENCE's own code only (linked
+// against the reference's util/crc32c.cc, never liblsbm_crc32c.so; built by
+// oracle/Makefile `dbbench_gpu` as oracle/_ref/db_verify).  TEST
+// INFRASTRUCTURE.
+//
+//   db_verify DIR [--open]
+//
+// Per table file (*.ldb): the footer, then EVERY block read through
+// the reference's ReadBlock with verify_checksums (table/format.cc:66-103) --
+// the index block, each data block it lists, the metaindex block and the
+// filter block it names -- and the entries of every data block counted.
+// Per log file (*.log, MANIFEST-*): every record read through the reference's
+// log::Reader with checksum = true (common/log_reader.cc:228-242), records
+// and reported corruptions counted.  With --open (on a copy: recovery writes),
+// the database is opened by the reference's DB::Open with paranoid_checks and
+// iterated with verify_checksums; the count of live entries and an FNV-1a
+// digest over (key, value) pairs in order identify its content.  One JSON line.
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "common/filename.h"
+#include "common/log_reader.h"
+#include "leveldb/comparator.h"
+#include "leveldb/db.h"
+#include "leveldb/env.h"
+#include "leveldb/iterator.h"
+#include "leveldb/options.h"
+#include "table/block.h"
+#include "table/format.h"
+
+using namespace leveldb;
+
+namespace {
+
+struct Counts {
+  uint64_t tables = 0, blocks = 0, entries = 0, table_errors = 0, unfinished = 0;
+  uint64_t logs = 0, records = 0, log_errors = 0, dropped_bytes = 0;
+  std::string first_error;
+  void error(const std::string& where, const Status& s) {
+    if (first_error.empty()) first_error = where + ": " + s.ToString();
+  }
+};
+
+// One block through ReadBlock with verification; `entries` counts its entries.
+Status VerifiedBlock(RandomAccessFile* f, const BlockHandle& h, std::vector<std::string>* values, uint64_t* entries) {
+  ReadOptions ro;
+  ro.verify_checksums = true;
+  BlockContents c;
+  Status s = ReadBlock(f, ro, h, &c);
+  if (!s.ok()) return s;
+  Block b(c);
+  Iterator* it = b.NewIterator(BytewiseComparator());
+  for (it->SeekToFirst(); it->Valid(); it->Next()) {
+    if (values) values->push_back(it->value().ToString());
+    if (entries) ++*entries;
+  }
+  s = it->status();
+  delete it;
+  return s;
+}
+
+// last: the highest-numbered table file, which the background thread may
+// have been writing when db_bench exited (it does not wait for it): a footer
+// that is not there yet marks it unfinished -- no manifest references it --
+// rather than corrupt.  (The reference's builder leaves the blocks written so
+// far; the GPU builder, which writes at Finish, an empty file.)
+void VerifyTable(Env* env, const std::string& path, bool last, Counts* n) {
+  uint64_t size = 0;
+  RandomAccessFile* f = nullptr;
+  Status s = env->GetFileSize(path, &size);
+  if (s.ok()) s = env->NewRandomAccessFile(path, &f);
+  char buf[Footer::kEncodedLength];
+  Slice in;
+  Footer footer;
+  if (s.ok() && size < Footer::kEncodedLength) s = Status::Corruption("file is too short to be an sstable");
+  if (s.ok()) s = f->Read(size - Footer::kEncodedLength, Footer::kEncodedLength, &in, buf);
+  if (s.ok()) s = footer.DecodeFrom(&in);
+  if (!s.ok() && last) {
+    n->unfinished++;
+    delete f;
+    return;
+  }
+  n->tables++;
+  std::vector<std::string> index, meta;
+  if (s.ok()) s = VerifiedBlock(f, footer.index_handle(), &index, nullptr);
+  if (s.ok()) n->blocks++;
+  for (size_t i = 0; s.ok() && i < index.size(); i++) {
+    Slice v(index[i]);
+    BlockHandle h;
+    s = h.DecodeFrom(&v);
+    if (s.ok()) s = VerifiedBlock(f, h, nullptr, &n->entries);
+    if (s.ok()) n->blocks++;
+  }
+  if (s.ok()) s = VerifiedBlock(f, footer.metaindex_handle(), &meta, nullptr);
+  if (s.ok()) n->blocks++;
+  for (size_t i = 0; s.ok() && i < meta.size(); i++) {  // the filter block(s)
+    Slice v(meta[i]);
+    BlockHandle h;
+    s = h.DecodeFrom(&v);
+    if (s.ok()) {
+      ReadOptions ro;
+      ro.verify_checksums = true;
+      BlockContents c;
+      s = ReadBlock(f, ro, h, &c);
+      if (s.ok() && c.heap_allocated) delete[] c.data.data();
+    }
+    if (s.ok()) n->blocks++;
+  }
+  if (!s.ok()) {
+    n->table_errors++;
+    n->error(path, s);
+  }
+  delete f;
+}
+
+struct LogReporter : public log::Reader::Reporter {
+  Counts* n;
+  std::string path;
+  void Corruption(size_t bytes, const Status& s) override {
+    n->log_errors++;
+    n->dropped_bytes += bytes;
+    n->error(path, s);
+  }
+};
+
+void VerifyLog(Env* env, const std::string& path, Counts* n) {
+  n->logs++;
+  SequentialFile* f = nullptr;
+  Status s = env->NewSequentialFile(path, &f);
+  if (!s.ok()) {
+    n->log_errors++;
+    n->error(path, s);
+    return;
+  }
+  LogReporter rep;
+  rep.n = n;
+  rep.path = path;
+  log::Reader reader(f, &rep, true /* checksum */, 0);
+  Slice rec;
+  std::string scratch;
+  while (reader.ReadRecord(&rec, &scratch)) n->records++;
+  delete f;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s DIR [--open]\n", argv[0]);
+    return 2;
+  }
+  const std::string dir = argv[1];
+  const bool open = argc > 2 && strcmp(argv[2], "--open") == 0;
+  Env* env = Env::Default();
+  std::vector<std::string> files;
+  Status s = env->GetChildren(dir, &files);
+  if (!s.ok()) {
+    fprintf(stderr, "%s\n", s.ToString().c_str());
+    return 1;
+  }
+  Counts n;
+  uint64_t last_table = 0;
+  for (size_t i = 0; i < files.size(); i++) {
+    uint64_t number;
+    FileType type;
+    if (ParseFileName(files[i], &number, &type) && type == kTableFile && number > last_table) last_table = number;
+  }
+  for (size_t i = 0; i < files.size(); i++) {
+    uint64_t number;
+    FileType type;
+    if (!ParseFileName(files[i], &number, &type)) continue;
+    const std::string path = dir + "/" + files[i];
+    if (type == kTableFile)
+      VerifyTable(env, path, number == last_table, &n);
+    else if (type == kLogFile || type == kDescriptorFile)
+      VerifyLog(env, path, &n);
+  }
+  uint64_t live = 0, digest = 1469598103934665603ull;  // FNV-1a 64
+  std::string open_error;
+  if (open) {
+    config::db_path = dir.c_str();  // (lsbm's global, set by db_bench's --db, lsbm/db_bench.cc:1802)
+    Options o;
+    o.paranoid_checks = true;
+    DB* db = nullptr;
+    s = DB::Open(o, dir, &db);
+    if (s.ok()) {
+      ReadOptions ro;
+      ro.verify_checksums = true;
+      Iterator* it = db->NewIterator(ro);
+      for (it->SeekToFirst(); it->Valid(); it->Next()) {
+        live++;
+        const Slice parts[2] = {it->key(), it->value()};
+        for (int p = 0; p < 2; p++) {
+          const uint64_t len = parts[p].size();
+          for (int k = 0; k < 8; k++) digest = (digest ^ ((len >> (8 * k)) & 0xff)) * 1099511628211ull;
+          for (size_t k = 0; k < parts[p].size(); k++)
+            digest = (digest ^ static_cast<uint8_t>(parts[p][k])) * 1099511628211ull;
+        }
+      }
+      s = it->status();
+      delete it;
+      delete db;
+    }
+    if (!s.ok()) open_error = s.ToString();
+  }
+  printf("{\"tables\": %llu, \"unfinished\": %llu, \"blocks\": %llu, \"entries\": %llu, \"table_errors\": %llu, \"logs\": %llu, "
+         "\"records\": %llu, \"log_errors\": %llu, \"dropped_bytes\": %llu, \"first_error\": \"%s\"",
+         (unsigned long long)n.tables, (unsigned long long)n.unfinished, (unsigned long long)n.blocks, (unsigned long long)n.entries,
+         (unsigned long long)n.table_errors, (unsigned long long)n.logs, (unsigned long long)n.records,
+         (unsigned long long)n.log_errors, (unsigned long long)n.dropped_bytes, n.first_error.c_str());
+  if (open)
+    printf(", \"live\": %llu, \"digest\": \"%016llx\", \"open_error\": \"%s\"", (unsigned long long)live,
+           (unsigned long long)digest, open_error.c_str());
+  printf("}\n");
+  return n.table_errors || n.log_errors || !open_error.empty() ? 1 : 0;
+}

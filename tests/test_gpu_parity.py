@@ -659,6 +659,58 @@ def test_compaction_end_to_end_with_both_gpu_ends_matches_the_reference(torch_cu
     assert int(f["input_blocks_verified"]) > 16000
 
 
+def test_db_bench_gpu_tables(torch_cuda, tmp_path):
+    """Config 1 end to end (BASELINE.json configs[0]):
+    lsbm's own db_bench, 1M writes, as shipped and as the Level-2 build
+    (oracle/Makefile dbbench_gpu: the same sources with
+    integration/table_builder_gpu.cc in place of table/table_builder.o and
+    Extend / Hash from liblsbm_crc32c.so), so every table lsbm's memtable
+    flushes and compactions write is sealed by one SealBlocks call on the GPU.
+    The reference-only checker (tests/cpp/db_verify.cc) reads every block of
+    every finished table and every WAL / MANIFEST record of the GPU-written
+    database with the reference's own CRC code, and opening it with
+    paranoid_checks gives the same content digest as the reference's database.
+    Finished tables that both runs wrote are byte-identical.  Skipped where the
+    binaries were not built."""
+    import hashlib
+    import os
+    import subprocess
+    from test_ref_link import db_bench_args, db_verify
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
+    if not all(os.access(os.path.join(ref, x), os.X_OK) for x in ("db_bench", "db_bench_gpu", "db_verify")):
+        pytest.skip("oracle/_ref/db_bench* not built (needs /root/reference at build time)")
+    runs = {}
+    for name in ("db_bench", "db_bench_gpu"):
+        db = tmp_path / name
+        db.mkdir()
+        env = dict(os.environ, LSBM_TABLE_STATS="1")
+        r = subprocess.run([os.path.join(ref, name)] + db_bench_args(str(db), 1_000_000),
+                           capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("separate")]
+        rc, v = db_verify(os.path.join(ref, "db_verify"), str(db))
+        assert rc == 0 and v["table_errors"] == 0 and v["log_errors"] == 0 and v["tables"] >= 8, v
+        rc, o = db_verify(os.path.join(ref, "db_verify"), str(db), str(tmp_path / (name + "_open")))
+        assert rc == 0 and o["open_error"] == "", o
+        stats = [ln for ln in r.stderr.splitlines() if ln.startswith("lsbm_table_stats")]
+        hashes = {}
+        for f in sorted(os.listdir(db)):
+            if f.endswith(".ldb"):
+                b = (db / f).read_bytes()
+                if len(b) >= 48 and b[-8:] == bytes.fromhex("57fb808b247547db"):  # a finished table
+                    hashes.setdefault(hashlib.sha256(b).hexdigest(), []).append(f)
+        runs[name] = dict(line=line, verify=v, digest=(o["live"], o["digest"]), stats=stats, hashes=hashes)
+        print(name, line, v, o["live"], o["digest"], stats)
+    assert runs["db_bench_gpu"]["digest"] == runs["db_bench"]["digest"]
+    # the GPU build sealed its tables on the GPU, the reference build has no such code
+    st = runs["db_bench_gpu"]["stats"]
+    assert st and int(st[0].split("tables_sealed_on_gpu=")[1].split()[0]) >= runs["db_bench_gpu"]["verify"]["tables"]
+    assert not runs["db_bench"]["stats"]
+    common = set(runs["db_bench"]["hashes"]) & set(runs["db_bench_gpu"]["hashes"])
+    print("finished tables byte-identical in both runs:", len(common), "of", len(runs["db_bench_gpu"]["hashes"]))
+    assert len(common) >= 1
+
+
 def test_cpp_block_compression_layer(torch_cuda, tmp_path):
     """include/lsbm/block_compression.h from C++: WriteBlock's compression and
     12.5% rule against the snappy oracle, ReadBlock's decompression and its

@@ -80,3 +80,65 @@ def test_gpu_table_builder_compiles_and_links_against_the_reference():
     assert any("SealBlocks" in u for u in undefined)  # from liblsbm_crc32c.so
     ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
     assert "liblsbm_crc32c.so" in ldd and "libamdhip64" in ldd
+
+
+# config 1 (BASELINE.json configs[0]): lsbm's own db_bench write workload
+# (SURVEY.md section 3.5), scaled by --writes
+DB_BENCH_ARGS = ["--benchmarks=separate", "--write_workload=counter", "--value_size=100", "--write_key_from=0",
+                 "--key_from=0", "--read_key_from=0", "--writespeed=-1", "--readspeed=0", "--random_reads=0",
+                 "--read_threads=0", "--countdown=600", "--block_cache_size=0", "--histogram=0"]
+
+
+def db_bench_args(db, writes):
+    return [f"--db={db}", f"--writes={writes}", f"--write_key_upto={writes}", f"--key_upto={writes}",
+            f"--read_key_upto={writes}"] + DB_BENCH_ARGS
+
+
+def db_verify(exe, db, open_copy=None):
+    """oracle/_ref/db_verify (reference code only) over a database directory:
+    its JSON line, and with open_copy the DB::Open digest of a copy."""
+    import json
+    import shutil
+    args = [exe, db]
+    if open_copy:
+        shutil.copytree(db, open_copy)
+        args = [exe, open_copy, "--open"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    return r.returncode, json.loads(line)
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "table")), reason="needs /root/reference")
+def test_db_bench_builds_three_ways_and_level1_writes_the_same_database(tmp_path):
+    """lsbm's db_bench from its own sources three ways (oracle/Makefile
+    dbbench_gpu): as shipped; Level 1 (this repo's util/crc32c.h first, its
+    Extend and Hash from liblsbm_crc32c.so); Level 2 (also
+    integration/table_builder_gpu.cc in place of table/table_builder.o).  Here,
+    without a GPU: the reference and the Level-1 build each run config 1 at
+    200K writes, and the reference-only checker (tests/cpp/db_verify.cc) reads
+    every block and log record of both databases with verification and finds
+    the same database content (DB::Open digest).  tests/test_gpu_parity.py runs
+    the Level-2 build on the GPU."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "dbbench_gpu"], check=True)
+    ref = os.path.join(REPO, "oracle", "_ref")
+    syms = subprocess.run(["nm", os.path.join(ref, "db_bench_gpu")], capture_output=True, text=True).stdout
+    assert " U _ZN7leveldb6crc32c6ExtendEjPKcm" in syms and " U _ZN7leveldb4HashEPKcmj" in syms
+    assert any("SealBlocks" in ln and " U " in ln for ln in syms.splitlines())
+    assert "_ZN7leveldb12TableBuilder6FinishEv" in syms
+    ldd = subprocess.run(["ldd", os.path.join(ref, "db_bench_l1")], capture_output=True, text=True).stdout
+    assert "liblsbm_crc32c.so" in ldd
+    digests = {}
+    for name in ("db_bench", "db_bench_l1"):
+        db = tmp_path / name
+        db.mkdir()
+        r = subprocess.run([os.path.join(ref, name)] + db_bench_args(str(db), 200_000),
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "separate" in r.stdout
+        rc, v = db_verify(os.path.join(ref, "db_verify"), str(db))
+        assert rc == 0 and v["table_errors"] == 0 and v["log_errors"] == 0, v
+        assert v["tables"] >= 1 and v["records"] > 0, v
+        rc, v = db_verify(os.path.join(ref, "db_verify"), str(db), str(tmp_path / (name + "_open")))
+        assert rc == 0 and v["open_error"] == "", v
+        digests[name] = (v["live"], v["digest"])
+    assert digests["db_bench"] == digests["db_bench_l1"]
