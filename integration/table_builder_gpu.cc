@@ -29,13 +29,15 @@
 // reference's own db_bench and DB code, this file, liblsbm_crc32c.so) and run
 // on the GPU by tests/test_gpu_parity.py (test_db_bench_gpu_tables).
 // LSBM_TABLE_DEVICE picks the HIP device (default 0); LSBM_TABLE_STATS=1
-// prints, at exit, how many tables and blocks were sealed on the GPU.
+// prints, at exit, how many tables and blocks were sealed on the GPU;
+// LSBM_TABLE_PREINIT=0 turns off opening the device at process start.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <thread>
 
 #include "integration/gpu_table_builder.h"
 #include "leveldb/cache.h"
@@ -68,6 +70,28 @@ void PrintStats() {
           (unsigned long long)g_tables.load(), (unsigned long long)g_blocks.load(),
           (unsigned long long)g_bytes.load());
 }
+
+// The device is opened when the process starts, on a thread of its own (one
+// seal of a one-block image: the HIP runtime, the device tables, a session and
+// the kernels' code), so that start-up overlaps the database's open and its
+// first memtable instead of stalling the first flush.  A binding inside lsbm
+// itself would do this in DB::Open.
+struct DeviceWarmup {
+  std::thread t;
+  DeviceWarmup() {
+    const char* e = getenv("LSBM_TABLE_PREINIT");
+    if (e && *e == '0') return;
+    t = std::thread([] {
+      char image[64] = {0};
+      const lsbm::BlockHandle h = {0, 16};
+      const uint8_t type = 0;
+      (void)lsbm::SealBlocks(TableDevice(), image, sizeof(image), &h, &type, 1);
+    });
+  }
+  ~DeviceWarmup() {
+    if (t.joinable()) t.join();
+  }
+} g_warmup;
 
 struct StatsAtExit {
   StatsAtExit() {

@@ -8,6 +8,8 @@
   l1    oracle/_ref/db_bench_l1   Level 1: Extend / Hash from liblsbm_crc32c.so
   gpu   oracle/_ref/db_bench_gpu  Level 2: also every table sealed on the GPU
                                   (integration/table_builder_gpu.cc)
+  gpu_noinit                      the same without opening the device at start
+                                  (LSBM_TABLE_PREINIT=0: the first flush opens it)
 
 Per run: db_bench's own report (micros/op of the writer thread over the 1M
 writes), the process's wall time and CPU time (user + sys of all its
@@ -33,15 +35,17 @@ REF = os.path.join(REPO, "oracle", "_ref")
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from test_ref_link import db_bench_args  # noqa: E402
 
-BUILDS = {"ref": "db_bench", "l1": "db_bench_l1", "gpu": "db_bench_gpu"}
+BUILDS = {"ref": ("db_bench", {}), "l1": ("db_bench_l1", {}), "gpu": ("db_bench_gpu", {}),
+          "gpu_noinit": ("db_bench_gpu", {"LSBM_TABLE_PREINIT": "0"})}
 
 
 def run(build, writes, scratch):
     db = tempfile.mkdtemp(prefix=f"dbab_{build}_", dir=scratch)
-    env = dict(os.environ, LSBM_TABLE_STATS="1")
+    exe, extra = BUILDS[build]
+    env = dict(os.environ, LSBM_TABLE_STATS="1", **extra)
     r0 = resource.getrusage(resource.RUSAGE_CHILDREN)
     t0 = time.perf_counter()
-    p = subprocess.Popen([os.path.join(REF, BUILDS[build])] + db_bench_args(db, writes),
+    p = subprocess.Popen([os.path.join(REF, exe)] + db_bench_args(db, writes),
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
     out, err = p.communicate(timeout=600)  # (reaped: its rusage is in RUSAGE_CHILDREN now)
     wall = time.perf_counter() - t0
