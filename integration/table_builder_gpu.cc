@@ -37,7 +37,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <thread>
+#include <vector>
 
 #include "integration/gpu_table_builder.h"
 #include "leveldb/cache.h"
@@ -63,29 +65,37 @@ std::atomic<uint64_t> g_size_hint(0);
 
 void DeletePreCachedBlock(const Slice&, void* value) { delete reinterpret_cast<Block*>(value); }
 
-std::atomic<uint64_t> g_tables(0), g_blocks(0), g_bytes(0);
+std::atomic<uint64_t> g_tables(0), g_blocks(0), g_bytes(0), g_finish_ns(0), g_finish_max_ns(0);
+const std::chrono::steady_clock::time_point g_start = std::chrono::steady_clock::now();
+std::atomic<uint64_t> g_warmup_ns(0), g_first_finish_ns(0);
 
 void PrintStats() {
-  fprintf(stderr, "lsbm_table_stats: tables_sealed_on_gpu=%llu blocks=%llu bytes=%llu\n",
+  fprintf(stderr,
+          "lsbm_table_stats: tables_sealed_on_gpu=%llu blocks=%llu bytes=%llu finish_ms_total=%.3f "
+          "finish_ms_max=%.3f warmup_ms=%.3f first_finish_at_ms=%.3f\n",
           (unsigned long long)g_tables.load(), (unsigned long long)g_blocks.load(),
-          (unsigned long long)g_bytes.load());
+          (unsigned long long)g_bytes.load(), g_finish_ns.load() * 1e-6, g_finish_max_ns.load() * 1e-6,
+          g_warmup_ns.load() * 1e-6, g_first_finish_ns.load() * 1e-6);
 }
 
 // The device is opened when the process starts, on a thread of its own (one
-// seal of a one-block image: the HIP runtime, the device tables, a session and
+// seal of a small image: the HIP runtime, the device tables, a session and
 // the kernels' code), so that start-up overlaps the database's open and its
 // first memtable instead of stalling the first flush.  A binding inside lsbm
 // itself would do this in DB::Open.
+constexpr size_t kWarmupBytes = 4096;
 struct DeviceWarmup {
   std::thread t;
   DeviceWarmup() {
     const char* e = getenv("LSBM_TABLE_PREINIT");
     if (e && *e == '0') return;
     t = std::thread([] {
-      char image[64] = {0};
-      const lsbm::BlockHandle h = {0, 16};
+      const auto t0 = std::chrono::steady_clock::now();
+      std::vector<char> image(kWarmupBytes);
+      const lsbm::BlockHandle h = {0, kWarmupBytes - 5};
       const uint8_t type = 0;
-      (void)lsbm::SealBlocks(TableDevice(), image, sizeof(image), &h, &type, 1);
+      (void)lsbm::SealBlocks(TableDevice(), image.data(), image.size(), &h, &type, 1);
+      g_warmup_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     });
   }
   ~DeviceWarmup() {
@@ -193,12 +203,21 @@ void TableBuilder::Flush(bool cache) {
 Status TableBuilder::status() const { return rep_->gpu.status(); }
 
 Status TableBuilder::Finish() {
-  const Status s = rep_->gpu.Finish();
+  const auto t0 = std::chrono::steady_clock::now();
+  uint64_t zero = 0;
+  g_first_finish_ns.compare_exchange_strong(
+      zero, std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - g_start).count());
+  const Status s = rep_->gpu.Finish();  // (the seal on the GPU and the file's one Append)
+  const uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   const uint64_t n = rep_->gpu.FileSize();
   if (s.ok()) {
     g_tables++;
     g_blocks += rep_->gpu.Blocks();
     g_bytes += n;
+    g_finish_ns += ns;
+    uint64_t m = g_finish_max_ns.load(std::memory_order_relaxed);
+    while (ns > m && !g_finish_max_ns.compare_exchange_weak(m, ns, std::memory_order_relaxed)) {
+    }
   }
   // remember the size for the next builder's image
   uint64_t prev = g_size_hint.load(std::memory_order_relaxed);
