@@ -20,6 +20,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <set>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,7 @@
 #include "leveldb/env.h"
 #include "leveldb/iterator.h"
 #include "leveldb/options.h"
+#include "lsbm/version_edit.h"
 #include "table/block.h"
 #include "table/format.h"
 
@@ -64,12 +66,13 @@ Status VerifiedBlock(RandomAccessFile* f, const BlockHandle& h, std::vector<std:
   return s;
 }
 
-// last: the highest-numbered table file, which the background thread may
-// have been writing when db_bench exited (it does not wait for it): a footer
-// that is not there yet marks it unfinished -- no manifest references it --
-// rather than corrupt.  (The reference's builder leaves the blocks written so
-// far; the GPU builder, which writes at Finish, an empty file.)
-void VerifyTable(Env* env, const std::string& path, bool last, Counts* n) {
+// listed: whether any MANIFEST edit added this table.  db_bench exits without
+// waiting for its background work, so tables being written at that moment
+// (a compaction's outputs, a memtable flush) are left unfinished, and no edit
+// names them: a missing footer there marks the file unfinished, not corrupt.
+// (The reference's builder leaves the blocks written so far; the GPU builder,
+// which writes at Finish, an empty file.)  A listed table must verify.
+void VerifyTable(Env* env, const std::string& path, bool listed, Counts* n) {
   uint64_t size = 0;
   RandomAccessFile* f = nullptr;
   Status s = env->GetFileSize(path, &size);
@@ -80,7 +83,7 @@ void VerifyTable(Env* env, const std::string& path, bool last, Counts* n) {
   if (s.ok() && size < Footer::kEncodedLength) s = Status::Corruption("file is too short to be an sstable");
   if (s.ok()) s = f->Read(size - Footer::kEncodedLength, Footer::kEncodedLength, &in, buf);
   if (s.ok()) s = footer.DecodeFrom(&in);
-  if (!s.ok() && last) {
+  if (!s.ok() && !listed) {
     n->unfinished++;
     delete f;
     return;
@@ -164,11 +167,29 @@ int main(int argc, char** argv) {
     return 1;
   }
   Counts n;
-  uint64_t last_table = 0;
+  // every table any MANIFEST edit added (lsbm/version_edit.h: four kinds of
+  // sorted tables), read with the reference's VersionEdit::DecodeFrom
+  std::set<uint64_t> listed;
   for (size_t i = 0; i < files.size(); i++) {
     uint64_t number;
     FileType type;
-    if (ParseFileName(files[i], &number, &type) && type == kTableFile && number > last_table) last_table = number;
+    if (!ParseFileName(files[i], &number, &type) || type != kDescriptorFile) continue;
+    SequentialFile* f = nullptr;
+    if (!env->NewSequentialFile(dir + "/" + files[i], &f).ok()) continue;
+    Counts ignore;
+    LogReporter rep;
+    rep.n = &ignore;
+    log::Reader reader(f, &rep, true, 0);
+    Slice rec;
+    std::string scratch;
+    while (reader.ReadRecord(&rec, &scratch)) {
+      VersionEdit edit;
+      if (!edit.DecodeFrom(rec).ok()) continue;
+      std::vector<std::pair<int, FileMetaData>>* added = edit.GetNewFiles();
+      for (int k = 0; k < 4; k++)
+        for (size_t j = 0; j < added[k].size(); j++) listed.insert(added[k][j].second.number);
+    }
+    delete f;
   }
   for (size_t i = 0; i < files.size(); i++) {
     uint64_t number;
@@ -176,7 +197,7 @@ int main(int argc, char** argv) {
     if (!ParseFileName(files[i], &number, &type)) continue;
     const std::string path = dir + "/" + files[i];
     if (type == kTableFile)
-      VerifyTable(env, path, number == last_table, &n);
+      VerifyTable(env, path, listed.count(number) != 0, &n);
     else if (type == kLogFile || type == kDescriptorFile)
       VerifyLog(env, path, &n);
   }
