@@ -29,8 +29,11 @@
 // reference's own db_bench and DB code, this file, liblsbm_crc32c.so) and run
 // on the GPU by tests/test_gpu_parity.py (test_db_bench_gpu_tables).
 // LSBM_TABLE_DEVICE picks the HIP device (default 0); LSBM_TABLE_STATS=1
-// prints, at exit, how many tables and blocks were sealed on the GPU;
-// LSBM_TABLE_PREINIT=0 turns off opening the device at process start.
+// prints, at exit, how many tables and blocks were sealed on the GPU and the
+// time Finish took (the first Finish of a process also opens the device: the
+// HIP runtime's start-up, 130-330 ms on the MI355X box, which opening the
+// device on a thread at process start did not hide -- db_bench's first flush
+// comes ~35-50 ms after start).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -38,8 +41,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <thread>
-#include <vector>
 
 #include "integration/gpu_table_builder.h"
 #include "leveldb/cache.h"
@@ -67,41 +68,17 @@ void DeletePreCachedBlock(const Slice&, void* value) { delete reinterpret_cast<B
 
 std::atomic<uint64_t> g_tables(0), g_blocks(0), g_bytes(0), g_finish_ns(0), g_finish_max_ns(0);
 const std::chrono::steady_clock::time_point g_start = std::chrono::steady_clock::now();
-std::atomic<uint64_t> g_warmup_ns(0), g_first_finish_ns(0);
+std::atomic<uint64_t> g_first_finish_ns(0);
 
 void PrintStats() {
   fprintf(stderr,
           "lsbm_table_stats: tables_sealed_on_gpu=%llu blocks=%llu bytes=%llu finish_ms_total=%.3f "
-          "finish_ms_max=%.3f warmup_ms=%.3f first_finish_at_ms=%.3f\n",
+          "finish_ms_max=%.3f first_finish_at_ms=%.3f\n",
           (unsigned long long)g_tables.load(), (unsigned long long)g_blocks.load(),
           (unsigned long long)g_bytes.load(), g_finish_ns.load() * 1e-6, g_finish_max_ns.load() * 1e-6,
-          g_warmup_ns.load() * 1e-6, g_first_finish_ns.load() * 1e-6);
+          g_first_finish_ns.load() * 1e-6);
 }
 
-// The device is opened when the process starts, on a thread of its own (one
-// seal of a small image: the HIP runtime, the device tables, a session and
-// the kernels' code), so that start-up overlaps the database's open and its
-// first memtable instead of stalling the first flush.  A binding inside lsbm
-// itself would do this in DB::Open.
-constexpr size_t kWarmupBytes = 4096;
-struct DeviceWarmup {
-  std::thread t;
-  DeviceWarmup() {
-    const char* e = getenv("LSBM_TABLE_PREINIT");
-    if (e && *e == '0') return;
-    t = std::thread([] {
-      const auto t0 = std::chrono::steady_clock::now();
-      std::vector<char> image(kWarmupBytes);
-      const lsbm::BlockHandle h = {0, kWarmupBytes - 5};
-      const uint8_t type = 0;
-      (void)lsbm::SealBlocks(TableDevice(), image.data(), image.size(), &h, &type, 1);
-      g_warmup_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-    });
-  }
-  ~DeviceWarmup() {
-    if (t.joinable()) t.join();
-  }
-} g_warmup;
 
 struct StatsAtExit {
   StatsAtExit() {

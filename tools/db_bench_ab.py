@@ -8,8 +8,6 @@
   l1    oracle/_ref/db_bench_l1   Level 1: Extend / Hash from liblsbm_crc32c.so
   gpu   oracle/_ref/db_bench_gpu  Level 2: also every table sealed on the GPU
                                   (integration/table_builder_gpu.cc)
-  gpu_noinit                      the same without opening the device at start
-                                  (LSBM_TABLE_PREINIT=0: the first flush opens it)
 
 Per run: db_bench's own report (micros/op of the writer thread over the 1M
 writes), the process's wall time and CPU time (user + sys of all its
@@ -35,8 +33,7 @@ REF = os.path.join(REPO, "oracle", "_ref")
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from test_ref_link import db_bench_args  # noqa: E402
 
-BUILDS = {"ref": ("db_bench", {}), "l1": ("db_bench_l1", {}), "gpu": ("db_bench_gpu", {}),
-          "gpu_noinit": ("db_bench_gpu", {"LSBM_TABLE_PREINIT": "0"})}
+BUILDS = {"ref": ("db_bench", {}), "l1": ("db_bench_l1", {}), "gpu": ("db_bench_gpu", {})}
 
 
 def run(build, writes, scratch):
