@@ -35,6 +35,7 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -56,8 +57,14 @@ class GpuTableBuilder {
   // size_hint: the table size the caller expects (a compaction knows its
   // MaxOutputFileSize): the image is reserved once instead of growing by
   // reallocation, each of which copies everything so far.
-  GpuTableBuilder(const Options& options, WritableFile* file, int device = 0, uint64_t size_hint = 0)
-      : options_(options),
+  // image: where the table image is built (cleared here; its capacity kept),
+  // so that a caller can hand the same buffer to table after table: its pages
+  // are then faulted in once, and may stay page-locked (table_builder_gpu.cc);
+  // null: a buffer of the builder's own.
+  GpuTableBuilder(const Options& options, WritableFile* file, int device = 0, uint64_t size_hint = 0,
+                  std::string* image = nullptr)
+      : image_(image ? *image : own_image_),
+        options_(options),
         index_options_(options),
         file_(file),
         device_(device),
@@ -66,9 +73,17 @@ class GpuTableBuilder {
         filter_(options.filter_policy ? new FilterBlockBuilder(options.filter_policy) : nullptr) {
     index_options_.block_restart_interval = 1;  // (every index entry a restart point)
     if (filter_) filter_->StartBlock(0);
-    if (size_hint) image_.reserve(size_hint + size_hint / 8 + (64u << 10));  // (+ meta blocks, the last block)
+    image_.clear();
+    const size_t want = ImageBytesFor(size_hint);
+    if (want > image_.capacity()) image_.reserve(want);  // (never smaller: reserve may shrink)
   }
   ~GpuTableBuilder() { delete filter_; }
+
+  // the image capacity reserved for a table of about size_hint bytes (+ the
+  // meta blocks and the last block)
+  static size_t ImageBytesFor(uint64_t size_hint) {
+    return size_hint ? size_hint + size_hint / 8 + (64u << 10) : 0;
+  }
 
   // TableBuilder::Add: keys in comparator order.
   void Add(const Slice& key, const Slice& value) {
@@ -106,6 +121,14 @@ class GpuTableBuilder {
   void SetDataBlockObserver(DataBlockObserver fn, void* arg) {
     observer_ = fn;
     observer_arg_ = arg;
+  }
+
+  // Called before the image buffer reallocates (it is about to move): a
+  // caller that page-locked the buffer unlocks it here.
+  typedef void (*ImageMoveObserver)(void* arg);
+  void SetImageMoveObserver(ImageMoveObserver fn, void* arg) {
+    move_observer_ = fn;
+    move_arg_ = arg;
   }
 
   // Closes the current data block (its trailer reserved, not computed).
@@ -152,6 +175,7 @@ class GpuTableBuilder {
       footer.set_index_handle(index_at);
       std::string tail;
       footer.EncodeTo(&tail);
+      Room(tail.size());
       image_.append(tail);
       status_ = file_->Append(image_);
     }
@@ -168,6 +192,13 @@ class GpuTableBuilder {
   const std::vector<lsbm::BlockHandle>& Handles() const { return handles_; }
 
  private:
+  // Capacity for `more` bytes; a reallocation (doubling) is announced first.
+  void Room(size_t more) {
+    if (image_.size() + more <= image_.capacity()) return;
+    if (move_observer_) move_observer_(move_arg_);
+    image_.reserve(std::max(2 * image_.capacity(), image_.size() + more));
+  }
+
   void AddIndexEntry() {
     std::string where;
     due_handle_.EncodeTo(&where);
@@ -198,10 +229,13 @@ class GpuTableBuilder {
     at->set_size(contents.size());
     handles_.push_back(lsbm::BlockHandle{image_.size(), contents.size()});
     types_.push_back(static_cast<uint8_t>(type));
+    Room(contents.size() + kBlockTrailerSize);
     image_.append(contents.data(), contents.size());
     image_.append(kBlockTrailerSize, '\0');
   }
 
+  std::string own_image_;
+  std::string& image_;  // the table so far: blocks with reserved trailers
   Options options_;
   Options index_options_;
   WritableFile* file_;
@@ -215,7 +249,6 @@ class GpuTableBuilder {
   bool index_due_ = false;  // a data block was closed and its index entry waits for the next key
   bool closed_ = false;
   BlockHandle due_handle_;
-  std::string image_;  // the table so far: blocks with reserved trailers
   std::string packed_;
   std::vector<lsbm::BlockHandle> handles_;  // every block of the image, for the seal
   std::vector<uint8_t> types_;
@@ -223,6 +256,8 @@ class GpuTableBuilder {
   bool closing_ = false;  // inside Finish
   DataBlockObserver observer_ = nullptr;
   void* observer_arg_ = nullptr;
+  ImageMoveObserver move_observer_ = nullptr;
+  void* move_arg_ = nullptr;
 
   GpuTableBuilder(const GpuTableBuilder&);
   void operator=(const GpuTableBuilder&);

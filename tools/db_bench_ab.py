@@ -8,6 +8,8 @@
   l1    oracle/_ref/db_bench_l1   Level 1: Extend / Hash from liblsbm_crc32c.so
   gpu   oracle/_ref/db_bench_gpu  Level 2: also every table sealed on the GPU
                                   (integration/table_builder_gpu.cc)
+  gpu_unlocked                    the same with the pooled images not kept
+                                  page-locked (LSBM_TABLE_REGISTER=0)
 
 Per run: db_bench's own report (micros/op of the writer thread over the 1M
 writes), the process's wall time and CPU time (user + sys of all its
