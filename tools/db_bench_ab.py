@@ -35,7 +35,8 @@ REF = os.path.join(REPO, "oracle", "_ref")
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from test_ref_link import db_bench_args  # noqa: E402
 
-BUILDS = {"ref": ("db_bench", {}), "l1": ("db_bench_l1", {}), "gpu": ("db_bench_gpu", {})}
+BUILDS = {"ref": ("db_bench", {}), "l1": ("db_bench_l1", {}), "gpu": ("db_bench_gpu", {}),
+          "gpu_unlocked": ("db_bench_gpu", {"LSBM_TABLE_REGISTER": "0"})}
 
 
 def run(build, writes, scratch):
