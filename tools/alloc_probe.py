@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""The fixed kernel over one 10M-block (40 GiB) batch allocated three ways
+(per-GPU rate of a config-5 shard):
+
+    python tools/alloc_probe.py [--blocks 10000000]
+
+  torch       torch.empty (the caching allocator's hipMalloc), as bench.py
+  hipMalloc   hipMalloc directly
+  contiguous  hipExtMallocWithFlags(..., hipDeviceMallocContiguous)
+
+Each: fill (splitmix64 0x5EED0000), 0.3 s spin-up, then 20 launches between
+HIP events; the 1M-block batch at each buffer's start for comparison; CRCs of
+the three checked equal.  One JSON line per case."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=10_000_000)
+    a = ap.parse_args()
+    import torch
+    from lsbm_amd import engine
+    from lsbm_amd._lib import lib
+    torch.cuda.set_device(0)
+    engine.init(0)
+    hip = ctypes.CDLL("libamdhip64.so")
+    L = 4096
+    n = a.blocks
+    nbytes = n * L
+    s = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(s.cuda_stream)
+    lb = lib()
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref = None
+    for how in ("torch", "hipMalloc", "contiguous"):
+        keep = None
+        if how == "torch":
+            keep = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            ptr = keep.data_ptr()
+        else:
+            p = ctypes.c_void_p()
+            if how == "hipMalloc":
+                rc = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes))
+            else:
+                rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x4))
+            if rc != 0:
+                print(json.dumps({"alloc": how, "error": rc}), flush=True)
+                continue
+            ptr = p.value
+        assert lb.lsbm_fill_splitmix64_dev(ctypes.c_void_p(ptr), nbytes, 0x5EED0000, sp) == 0
+        for m in (n, 1 << 20):
+            def launch():
+                assert lb.lsbm_crc32c_fixed_dev(ctypes.c_void_p(ptr), L, L, m, None,
+                                                ctypes.c_void_p(out.data_ptr()), 0, sp) == 0
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.3:
+                launch()
+                torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(20):
+                launch()
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            if m == n:
+                crc = out.cpu()
+                same = True if ref is None else bool(torch.equal(crc, ref))
+                ref = crc if ref is None else ref
+            print(json.dumps({"alloc": how, "blocks": m, "ms": round(ms, 4),
+                              "GiBps": round(m * L / (ms / 1e3) / 2**30, 1),
+                              "pct_8TBs": round(100 * m * L / (ms / 1e3) / 8e12, 2),
+                              "crcs_equal_torch": same if m == n else None}), flush=True)
+        del keep
+        if how != "torch":
+            hip.hipFree(ctypes.c_void_p(ptr))
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
