@@ -525,7 +525,9 @@ def test_cpp_concurrent_table_callers(torch_cuda, tmp_path, pinned, zero_copy_mb
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK"), r.stdout
     speedup = float(r.stdout.split("speedup=")[1].split()[0])
-    assert speedup >= (1.1 if pinned == 0 and auto_lock == "0" else 0.95), r.stdout
+    # (page-locked: 1.05-1.18 once the registrations of disjoint images ran in
+    # parallel, profiles/r05/lock_parallel/; 0.80 while they were serialised)
+    assert speedup >= (1.1 if pinned == 0 and auto_lock == "0" else 0.9), r.stdout
 
 
 @pytest.mark.parametrize("auto_lock", ["1", "0"], ids=["auto-lock", "staged"])
