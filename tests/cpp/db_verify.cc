@@ -48,10 +48,12 @@ struct Counts {
   }
 };
 
-// One block through ReadBlock with verification; `entries` counts its entries.
-Status VerifiedBlock(RandomAccessFile* f, const BlockHandle& h, std::vector<std::string>* values, uint64_t* entries) {
+// One block's entries (values kept when asked for, counted into `entries`),
+// read through ReadBlock with or without verify_checksums.
+Status ReadEntries(RandomAccessFile* f, const BlockHandle& h, bool verify, std::vector<std::string>* values,
+                   uint64_t* entries) {
   ReadOptions ro;
-  ro.verify_checksums = true;
+  ro.verify_checksums = verify;
   BlockContents c;
   Status s = ReadBlock(f, ro, h, &c);
   if (!s.ok()) return s;
@@ -72,7 +74,14 @@ Status VerifiedBlock(RandomAccessFile* f, const BlockHandle& h, std::vector<std:
 // names them: a missing footer there marks the file unfinished, not corrupt.
 // (The reference's builder leaves the blocks written so far; the GPU builder,
 // which writes at Finish, an empty file.)  A listed table must verify.
-void VerifyTable(Env* env, const std::string& path, bool listed, Counts* n) {
+// Every block the verifying reader would check -- the index block, each data
+// block, the metaindex block and the blocks it names (the filter) -- goes
+// through ReadBlock with verify_checksums; one that fails with a checksum
+// mismatch is listed in `bad` as "file:offset" and the walk goes on (the
+// index and metaindex are parsed unverified, as Table::Open reads them).
+void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool listed, Counts* n,
+                 std::vector<std::string>* bad) {
+  const std::string path = dir + "/" + name;
   uint64_t size = 0;
   RandomAccessFile* f = nullptr;
   Status s = env->GetFileSize(path, &size);
@@ -89,30 +98,48 @@ void VerifyTable(Env* env, const std::string& path, bool listed, Counts* n) {
     return;
   }
   n->tables++;
+  // one block checked: a checksum mismatch is listed, anything else stops the table
+  auto check = [&](const BlockHandle& h, std::vector<std::string>* values, uint64_t* entries) {
+    Status v = ReadEntries(f, h, true, values, entries);
+    n->blocks++;
+    if (v.ok()) return true;
+    if (v.ToString().find("block checksum mismatch") != std::string::npos) {
+      bad->push_back(name + ":" + std::to_string(h.offset()));
+      return true;
+    }
+    s = v;
+    return false;
+  };
   std::vector<std::string> index, meta;
-  if (s.ok()) s = VerifiedBlock(f, footer.index_handle(), &index, nullptr);
-  if (s.ok()) n->blocks++;
-  for (size_t i = 0; s.ok() && i < index.size(); i++) {
-    Slice v(index[i]);
-    BlockHandle h;
-    s = h.DecodeFrom(&v);
-    if (s.ok()) s = VerifiedBlock(f, h, nullptr, &n->entries);
-    if (s.ok()) n->blocks++;
+  if (s.ok()) s = ReadEntries(f, footer.index_handle(), false, &index, nullptr);
+  if (s.ok() && check(footer.index_handle(), nullptr, nullptr)) {
+    for (size_t i = 0; s.ok() && i < index.size(); i++) {
+      Slice v(index[i]);
+      BlockHandle h;
+      s = h.DecodeFrom(&v);
+      if (s.ok()) check(h, nullptr, &n->entries);
+    }
   }
-  if (s.ok()) s = VerifiedBlock(f, footer.metaindex_handle(), &meta, nullptr);
-  if (s.ok()) n->blocks++;
-  for (size_t i = 0; s.ok() && i < meta.size(); i++) {  // the filter block(s)
-    Slice v(meta[i]);
-    BlockHandle h;
-    s = h.DecodeFrom(&v);
-    if (s.ok()) {
+  if (s.ok()) s = ReadEntries(f, footer.metaindex_handle(), false, &meta, nullptr);
+  if (s.ok() && check(footer.metaindex_handle(), nullptr, nullptr)) {
+    for (size_t i = 0; s.ok() && i < meta.size(); i++) {  // the filter block(s): raw bytes, verified
+      Slice v(meta[i]);
+      BlockHandle h;
+      s = h.DecodeFrom(&v);
+      if (!s.ok()) break;
       ReadOptions ro;
       ro.verify_checksums = true;
       BlockContents c;
-      s = ReadBlock(f, ro, h, &c);
-      if (s.ok() && c.heap_allocated) delete[] c.data.data();
+      Status r = ReadBlock(f, ro, h, &c);
+      n->blocks++;
+      if (r.ok()) {
+        if (c.heap_allocated) delete[] c.data.data();
+      } else if (r.ToString().find("block checksum mismatch") != std::string::npos) {
+        bad->push_back(name + ":" + std::to_string(h.offset()));
+      } else {
+        s = r;
+      }
     }
-    if (s.ok()) n->blocks++;
   }
   if (!s.ok()) {
     n->table_errors++;
@@ -167,6 +194,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   Counts n;
+  std::vector<std::string> bad;  // every block that fails its checksum, "file:offset"
   // every table any MANIFEST edit added (lsbm/version_edit.h: four kinds of
   // sorted tables), read with the reference's VersionEdit::DecodeFrom
   std::set<uint64_t> listed;
@@ -197,7 +225,7 @@ int main(int argc, char** argv) {
     if (!ParseFileName(files[i], &number, &type)) continue;
     const std::string path = dir + "/" + files[i];
     if (type == kTableFile)
-      VerifyTable(env, path, listed.count(number) != 0, &n);
+      VerifyTable(env, dir, files[i], listed.count(number) != 0, &n, &bad);
     else if (type == kLogFile || type == kDescriptorFile)
       VerifyLog(env, path, &n);
   }
@@ -234,9 +262,12 @@ int main(int argc, char** argv) {
          (unsigned long long)n.tables, (unsigned long long)n.unfinished, (unsigned long long)n.blocks, (unsigned long long)n.entries,
          (unsigned long long)n.table_errors, (unsigned long long)n.logs, (unsigned long long)n.records,
          (unsigned long long)n.log_errors, (unsigned long long)n.dropped_bytes, n.first_error.c_str());
+  printf(", \"bad_blocks\": [");
+  for (size_t i = 0; i < bad.size(); i++) printf("%s\"%s\"", i ? ", " : "", bad[i].c_str());
+  printf("]");
   if (open)
     printf(", \"live\": %llu, \"digest\": \"%016llx\", \"open_error\": \"%s\"", (unsigned long long)live,
            (unsigned long long)digest, open_error.c_str());
   printf("}\n");
-  return n.table_errors || n.log_errors || !open_error.empty() ? 1 : 0;
+  return n.table_errors || n.log_errors || !bad.empty() || !open_error.empty() ? 1 : 0;
 }

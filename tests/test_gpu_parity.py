@@ -713,6 +713,62 @@ def test_db_bench_gpu_tables(torch_cuda, tmp_path):
     assert len(common) >= 1
 
 
+def test_db_check_gpu_matches_the_reference_on_a_db_bench_database(torch_cuda, tmp_path):
+    """A whole lsbm database, written by the reference's own db_bench (config
+    1, 1M writes), checked two ways: tools/db_check_gpu.cc (this repo's layers
+    only: every table's blocks in ONE VerifyTables call, each log through
+    BatchReader) and oracle/_ref/db_verify (the reference's ReadBlock and
+    log::Reader with its own CRC code).  Clean, both find nothing; then with
+    bytes flipped in data blocks of three tables and in the WAL, both list the
+    SAME failing blocks (file:offset) and the same reporter calls and dropped
+    bytes, with the tables mapped read-only (staged) and read into heap
+    buffers (page-locked in place).  Skipped where the reference binaries were
+    not built."""
+    import os
+    import shutil
+    import subprocess
+    from test_ref_link import db_bench_args, db_check_gpu, db_verify
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
+    if not all(os.access(os.path.join(ref, x), os.X_OK) for x in ("db_bench", "db_verify")):
+        pytest.skip("oracle/_ref/db_bench, db_verify not built (needs /root/reference at build time)")
+    db = tmp_path / "db"
+    db.mkdir()
+    r = subprocess.run([os.path.join(ref, "db_bench")] + db_bench_args(str(db), 1_000_000),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, v = db_verify(os.path.join(ref, "db_verify"), str(db))
+    g = db_check_gpu(str(db), "0", tmp_path)
+    print("clean", v, g)
+    assert rc == 0 and v["bad_blocks"] == [] and g["bad_blocks"] == []
+    assert (g["tables"], g["blocks"], g["records"]) == (v["tables"], v["blocks"], v["records"])
+    assert g["log_corruptions"] == v["log_errors"] == 0
+    # corrupt a copy: one byte in the data region of three finished tables
+    # (inside some data block or its trailer), one in the middle of the WAL
+    bad = tmp_path / "bad"
+    shutil.copytree(db, bad)
+    finished = sorted(f for f in os.listdir(bad) if f.endswith(".ldb") and os.path.getsize(bad / f) > (1 << 20)
+                      and (bad / f).read_bytes()[-8:] == bytes.fromhex("57fb808b247547db"))
+    assert len(finished) >= 3
+    for k, f in enumerate(finished[:3]):
+        b = bytearray((bad / f).read_bytes())
+        for at in (4096 * (k + 1) + 7, len(b) // 3 + 1000 * k):
+            b[at] ^= 0x10
+        (bad / f).write_bytes(bytes(b))
+    logs = [f for f in os.listdir(bad) if f.endswith(".log") and os.path.getsize(bad / f) > 100_000]
+    assert logs
+    b = bytearray((bad / logs[0]).read_bytes())
+    b[len(b) // 2] ^= 0x01
+    (bad / logs[0]).write_bytes(bytes(b))
+    rc, v = db_verify(os.path.join(ref, "db_verify"), str(bad))
+    assert len(v["bad_blocks"]) == 6, v
+    for read in ("mmap", "heap"):  # (read-only mappings staged; heap images page-locked in place)
+        g = db_check_gpu(str(bad), "0", tmp_path, *(["--read=heap"] if read == "heap" else []))
+        print("corrupted", read, v, g)
+        assert sorted(g["bad_blocks"]) == sorted(v["bad_blocks"])
+        assert g["log_corruptions"] == v["log_errors"] >= 1
+        assert g["dropped_bytes"] == v["dropped_bytes"] and g["records"] == v["records"]
+
+
 def test_cpp_block_compression_layer(torch_cuda, tmp_path):
     """include/lsbm/block_compression.h from C++: WriteBlock's compression and
     12.5% rule against the snappy oracle, ReadBlock's decompression and its

@@ -108,6 +108,21 @@ def db_verify(exe, db, open_copy=None):
     return r.returncode, json.loads(line)
 
 
+def db_check_gpu(db, arg, tmp_path, *more):
+    """tools/db_check_gpu.cc (this repo's layers only), built once per test, over
+    a database directory: its JSON line."""
+    import json
+    exe = tmp_path / "db_check_gpu"
+    if not exe.exists():
+        lib = os.path.join(REPO, "lsbm_amd")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(REPO, "include"),
+                        os.path.join(REPO, "tools", "db_check_gpu.cc"), "-L", lib, "-llsbm_crc32c",
+                        "-Wl,-rpath," + lib, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), db, arg, *more], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "table")), reason="needs /root/reference")
 def test_db_bench_builds_three_ways_and_level1_writes_the_same_database(tmp_path):
     """lsbm's db_bench from its own sources three ways (oracle/Makefile
@@ -138,6 +153,9 @@ def test_db_bench_builds_three_ways_and_level1_writes_the_same_database(tmp_path
         rc, v = db_verify(os.path.join(ref, "db_verify"), str(db))
         assert rc == 0 and v["table_errors"] == 0 and v["log_errors"] == 0, v
         assert v["tables"] >= 1 and v["records"] > 0, v
+        # tools/db_check_gpu.cc gathers the same blocks (its own footer / block parsing)
+        g = db_check_gpu(str(db), "--parse-only", tmp_path)
+        assert (g["tables"], g["unfinished"], g["blocks"]) == (v["tables"], v["unfinished"], v["blocks"]), (g, v)
         rc, v = db_verify(os.path.join(ref, "db_verify"), str(db), str(tmp_path / (name + "_open")))
         assert rc == 0 and v["open_error"] == "", v
         digests[name] = (v["live"], v["digest"])
