@@ -36,6 +36,7 @@
 #include <string>
 #include <vector>
 
+#include "integration/image_pool.h"
 #include "leveldb/env.h"
 #include "leveldb/iterator.h"
 #include "leveldb/options.h"
@@ -50,11 +51,22 @@ namespace leveldb {
 // reads return pointers into it (ReadBlock then uses them in place,
 // table/format.cc:105-112).  The buffer is `new char[]` (no zero fill: the
 // file's bytes are read straight into it), writable heap memory, so
-// VerifyBlocks page-locks it for its call.
+// VerifyBlocks page-locks it for its call; or a pooled image, page-locked
+// already once it has been used.
 class TableImageFile : public RandomAccessFile {
  public:
-  explicit TableImageFile(uint64_t size) : data_(new char[size ? size : 1]), size_(size) {}
-  ~TableImageFile() { delete[] data_; }
+  explicit TableImageFile(uint64_t size) : own_(new char[size ? size : 1]), data_(own_), size_(size) {}
+  // An image from `pool` (integration/image_pool.h), back to it with this
+  // file: its pages stay faulted in and page-locked from table to table.
+  TableImageFile(uint64_t size, ImagePool* pool) : pool_(pool), pooled_(pool->Take(size ? size : 1)), size_(size) {
+    std::string& b = pooled_->bytes;
+    if (b.size() < size) b.resize(size);  // (within its capacity: the image does not move)
+    data_ = &b[0];
+  }
+  ~TableImageFile() {
+    if (pooled_) pool_->Give(pooled_);
+    delete[] own_;
+  }
   Status Read(uint64_t offset, size_t n, Slice* result, char*) const {
     if (offset > size_) return Status::IOError("table image", "read past the end");
     *result = Slice(data_ + offset, std::min<uint64_t>(n, size_ - offset));
@@ -64,6 +76,9 @@ class TableImageFile : public RandomAccessFile {
   uint64_t size() const { return size_; }
 
  private:
+  char* own_ = nullptr;
+  ImagePool* pool_ = nullptr;
+  PooledImage* pooled_ = nullptr;
   char* data_;
   uint64_t size_;
   TableImageFile(const TableImageFile&);
@@ -74,14 +89,16 @@ class TableImageFile : public RandomAccessFile {
 // block on HIP device `device` in one call, and on success opens *table over
 // it (the caller deletes the table, then the image file).  *data_blocks
 // receives the number of blocks verified.
+// pool (optional): the image comes from it (integration/image_pool.h) and
+// goes back when *image_file is deleted.
 inline Status OpenVerifiedTable(const Options& options, uint64_t file_number, RandomAccessFile* file,
                                 uint64_t size, int device, TableImageFile** image_file, Table** table,
-                                size_t* data_blocks) {
+                                size_t* data_blocks, ImagePool* pool = nullptr) {
   *table = nullptr;
   *image_file = nullptr;
   *data_blocks = 0;
   if (size < Footer::kEncodedLength) return Status::InvalidArgument("file is too short to be an sstable");
-  TableImageFile* f = new TableImageFile(size);
+  TableImageFile* f = pool ? new TableImageFile(size, pool) : new TableImageFile(size);
   Slice got;
   Status s = file->Read(0, size, &got, f->data());
   if (s.ok() && got.size() != size) s = Status::Corruption("truncated block read");

@@ -41,12 +41,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <mutex>
-#include <vector>
-
-#include <hip/hip_runtime_api.h>
 
 #include "integration/gpu_table_builder.h"
+#include "integration/image_pool.h"
 #include "leveldb/cache.h"
 #include "leveldb/comparator.h"
 #include "leveldb/table_builder.h"
@@ -67,88 +64,6 @@ int TableDevice() {
 // regrowth copies the image so far).  A compaction's outputs are all near its
 // MaxOutputFileSize; BuildTable's are one memtable each.
 std::atomic<uint64_t> g_size_hint(0);
-
-// Table images, reused from table to table.  A fresh multi-MiB std::string
-// per table is fresh mmap-ed memory each time: every page faults in while the
-// table is built, is page-locked by SealBlocks for its call, unlocked, and
-// unmapped after the one Append -- measured on db_bench (10M writes, 340
-// tables): +1.5-2 s of host CPU against the reference, its writer 20% slower.
-// A pooled image keeps its pages, and (LSBM_TABLE_REGISTER, default on) stays
-// page-locked with hipHostRegister from the table that grew it on, so a seal
-// DMAs it in place with no per-call lock.  At most as many images as builders
-// run at once (lsbm: a memtable flush and a compaction).
-struct PooledImage {
-  std::string bytes;
-  void* registered = nullptr;  // the range page-locked for it, if any
-  size_t registered_bytes = 0;
-};
-
-bool RegisterImages() {
-  static const bool on = [] {
-    const char* e = getenv("LSBM_TABLE_REGISTER");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
-class ImagePool {
- public:
-  // an image with room for `bytes` (grown here, unlocked first, so that the
-  // builder's constructor does not move it)
-  PooledImage* Take(size_t bytes) {
-    PooledImage* p = nullptr;
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      if (!free_.empty()) {
-        p = free_.back();
-        free_.pop_back();
-      }
-    }
-    if (!p) p = new PooledImage();
-    if (bytes > p->bytes.capacity()) {
-      Moving(p);
-      p->bytes.reserve(bytes);
-    }
-    return p;
-  }
-  // the image is about to move (a table outgrew it): unlock it first
-  static void Moving(void* arg) {
-    PooledImage* p = static_cast<PooledImage*>(arg);
-    if (p->registered) (void)hipHostUnregister(p->registered);
-    p->registered = nullptr;
-    p->registered_bytes = 0;
-  }
-  // back into the pool after Finish / Abandon: page-locked at its current
-  // address and capacity
-  void Give(PooledImage* p) {
-    if (RegisterImages() && p->bytes.capacity() >= (1u << 20)) {
-      void* at = &p->bytes[0];
-      const size_t n = p->bytes.capacity();
-      if (p->registered != at || p->registered_bytes != n) {
-        if (p->registered) (void)hipHostUnregister(p->registered);
-        p->registered = nullptr;
-        p->registered_bytes = 0;
-        if (hipHostRegister(at, n, hipHostRegisterDefault) == hipSuccess) {
-          p->registered = at;
-          p->registered_bytes = n;
-        } else {
-          (void)hipGetLastError();
-        }
-      }
-    }
-    std::lock_guard<std::mutex> l(mu_);
-    free_.push_back(p);
-  }
-
- private:
-  std::mutex mu_;
-  std::vector<PooledImage*> free_;  // (kept until exit: process teardown releases them)
-};
-
-ImagePool& Images() {
-  static ImagePool* pool = new ImagePool();
-  return *pool;
-}
 
 void DeletePreCachedBlock(const Slice&, void* value) { delete reinterpret_cast<Block*>(value); }
 
@@ -181,12 +96,12 @@ struct TableBuilder::Rep {
         options(opt),
         file(f),
         hint(g_size_hint.load(std::memory_order_relaxed)),
-        image(Images().Take(GpuTableBuilder::ImageBytesFor(hint))),
+        image(ImagePool::Default().Take(GpuTableBuilder::ImageBytesFor(hint))),
         gpu(opt, f, TableDevice(), hint, &image->bytes) {
     gpu.SetDataBlockObserver(&Rep::Observe, this);
     gpu.SetImageMoveObserver(&ImagePool::Moving, image);
   }
-  ~Rep() { Images().Give(image); }
+  ~Rep() { ImagePool::Default().Give(image); }  // (pooled and kept page-locked: integration/image_pool.h)
 
   static void Observe(void* arg, const Slice& contents, bool closing) {
     Rep* r = static_cast<Rep*>(arg);

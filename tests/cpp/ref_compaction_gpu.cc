@@ -37,6 +37,7 @@
 #include "common/dbformat.h"
 #include "integration/gpu_table_builder.h"
 #include "integration/gpu_table_reader.h"
+#include "integration/image_pool.h"
 #include "leveldb/env.h"
 #include "leveldb/filter_policy.h"
 #include "leveldb/iterator.h"
@@ -108,9 +109,35 @@ template <>
 TableBuilder* make_builder<TableBuilder>(const Options& opt, WritableFile* f, uint64_t) {
   return new TableBuilder(opt, f);
 }
+// The GPU ends build into pooled images (integration/image_pool.h: kept
+// faulted in and page-locked from table to table) unless LSBM_POOL_IMAGES=0.
+bool pool_images() {
+  static const bool on = [] {
+    const char* e = getenv("LSBM_POOL_IMAGES");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+struct PooledGpuTableBuilder {
+  PooledImage* image;
+  GpuTableBuilder b;
+  PooledGpuTableBuilder(const Options& opt, WritableFile* f, uint64_t target)
+      : image(ImagePool::Default().Take(GpuTableBuilder::ImageBytesFor(target))),
+        b(opt, f, 0, target, &image->bytes) {
+    b.SetImageMoveObserver(&ImagePool::Moving, image);
+  }
+  ~PooledGpuTableBuilder() { ImagePool::Default().Give(image); }
+  void Add(const Slice& k, const Slice& v) { b.Add(k, v); }
+  Status Finish() { return b.Finish(); }
+  uint64_t FileSize() const { return b.FileSize(); }
+};
 template <>
 GpuTableBuilder* make_builder<GpuTableBuilder>(const Options& opt, WritableFile* f, uint64_t target) {
   return new GpuTableBuilder(opt, f, 0, target);
+}
+template <>
+PooledGpuTableBuilder* make_builder<PooledGpuTableBuilder>(const Options& opt, WritableFile* f, uint64_t target) {
+  return new PooledGpuTableBuilder(opt, f, target);
 }
 
 // Runs the merge of `children` into tables of about `target` bytes, through
@@ -231,14 +258,16 @@ int main(int argc, char** argv) {
     for (int j = 0; j < K; j++) {
       srcs.push_back(new StringSource(inputs[j]));
       size_t nb = 0;
-      EXPECT(OpenVerifiedTable(opt, 20 + j, srcs.back(), inputs[j].size(), 0, &imfs[j], &gtabs[j], &nb).ok());
+      EXPECT(OpenVerifiedTable(opt, 20 + j, srcs.back(), inputs[j].size(), 0, &imfs[j], &gtabs[j], &nb,
+                               pool_images() ? &ImagePool::Default() : nullptr).ok());
       verified += nb;
       ReadOptions fast;  // (verified above)
       fast.fill_cache = false;
       gits.push_back(gtabs[j]->NewIterator(fast));
     }
     gs = Status::OK();
-    gpu_out = merge_into_tables<GpuTableBuilder>(opt, gits.data(), K, out_bytes, &gs);
+    gpu_out = pool_images() ? merge_into_tables<PooledGpuTableBuilder>(opt, gits.data(), K, out_bytes, &gs)
+                            : merge_into_tables<GpuTableBuilder>(opt, gits.data(), K, out_bytes, &gs);
     gpu_ms[round] = (now() - t2) * 1e3;
     gpu_cpu[round] = (cpu_now() - c2) * 1e3;
     for (Table* t : gtabs) delete t;
@@ -266,10 +295,10 @@ int main(int argc, char** argv) {
 #endif
   printf("%s cpu_side=%s inputs=%d input_bytes=%llu entries=%llu input_blocks_verified=%zu outputs=%zu identical=%zu "
          "output_bytes=%llu cpu_ms=%.1f gpu_ends_ms=%.1f speedup=%.2f cpu_side_cpu_ms=%.1f gpu_ends_cpu_ms=%.1f "
-         "first_round_ms=%.1f/%.1f\n",
+         "first_round_ms=%.1f/%.1f pooled_images=%d\n",
          fails ? "FAILED" : "OK", cpu_side, K, (unsigned long long)in_total, (unsigned long long)total_entries,
          verified, ref_out.size(), identical, (unsigned long long)out_total, ref_steady, gpu_steady,
-         ref_steady / gpu_steady, ref_cpu_s, gpu_cpu_s, ref_ms[0], gpu_ms[0]);
+         ref_steady / gpu_steady, ref_cpu_s, gpu_cpu_s, ref_ms[0], gpu_ms[0], (int)pool_images());
   delete bloom;
   (void)lsbm_crc32c_shutdown();
   return fails ? 1 : 0;
