@@ -7,6 +7,7 @@
   torch       torch.empty (the caching allocator's hipMalloc), as bench.py
   hipMalloc   hipMalloc directly
   contiguous  hipExtMallocWithFlags(..., hipDeviceMallocContiguous)
+  chunks      the same blocks as 1M-block allocations, one launch each
 
 Each: fill (splitmix64 0x5EED0000), 0.3 s spin-up, then 20 launches between
 HIP events; the 1M-block batch at each buffer's start for comparison; CRCs of
@@ -83,6 +84,33 @@ def main():
             hip.hipFree(ctypes.c_void_p(ptr))
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+
+    # the same blocks held as ten separate 1M-block allocations, one launch each
+    chunks = []
+    for c in range((n + (1 << 20) - 1) >> 20):
+        m = min(1 << 20, n - (c << 20))
+        t = torch.empty(m * L, dtype=torch.uint8, device="cuda")
+        assert lb.lsbm_fill_splitmix64_dev(ctypes.c_void_p(t.data_ptr()), m * L, 0x5EED0000 + (c << 20) * (L // 8), sp) == 0
+        chunks.append((t, m))
+    def launch_all():
+        for c, (t, m) in enumerate(chunks):
+            assert lb.lsbm_crc32c_fixed_dev(ctypes.c_void_p(t.data_ptr()), L, L, m, None,
+                                            ctypes.c_void_p(out.data_ptr() + 4 * (c << 20)), 0, sp) == 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        launch_all()
+        torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(20):
+        launch_all()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    same = bool(torch.equal(out.cpu(), ref)) if ref is not None else None
+    print(json.dumps({"alloc": "torch, 1M-block chunks", "blocks": n, "ms": round(ms, 4),
+                      "GiBps": round(n * L / (ms / 1e3) / 2**30, 1), "pct_8TBs": round(100 * n * L / (ms / 1e3) / 8e12, 2),
+                      "crcs_equal_torch": same}), flush=True)
 
 
 if __name__ == "__main__":
