@@ -83,7 +83,13 @@ void build_consts(DevConsts* c) {
     gf2::nibble_tables(p, c->pow_nib[k]);
     p = gf2::mul(p, p);
   }
-  for (int z = 0; z < 128; z++) gf2::nibble_tables(gf2::byte_pow(-z), c->neg_nib[z]);
+  // (powers built one step from the last, not each by squaring: the device's
+  // set-up is then ~1 ms of host work instead of ~15)
+  const gf2::Mat inv1 = gf2::byte_pow(-1), fwd1 = gf2::byte_pow(1);
+  {
+    gf2::Mat m = gf2::identity();
+    for (int z = 0; z < 128; z++, m = gf2::mul(inv1, m)) gf2::nibble_tables(m, c->neg_nib[z]);
+  }
   gf2::nibble_tables(gf2::byte_pow(-4), c->neg4_nib);
   for (int li = 0; li < 8; li++) gf2::nibble_tables(gf2::byte_pow(116 - 16 * li), c->fin_nib[li]);
   // LDS image (layout: crc32c_device.h header comment)
@@ -125,8 +131,10 @@ void build_consts(DevConsts* c) {
       for (uint32_t b = 0; b < 16; b++)
         if (b >= lo && b < hi) c->lds_image[kStreamHM / 4 + t * 4 + b / 4] |= 0xffu << (8 * (b % 4));
     }
-  for (uint32_t d = 0; d < 128; d++)  // stream kernel: ~0 injected d bytes before the row start
-    c->lds_image[kStreamR0 / 4 + d] = gf2::apply(gf2::byte_pow(-(int64_t)d), 0xffffffffu);
+  {
+    uint32_t v = 0xffffffffu;  // stream kernel: ~0 injected d bytes before the row start
+    for (uint32_t d = 0; d < 128; d++, v = gf2::apply(inv1, v)) c->lds_image[kStreamR0 / 4 + d] = v;
+  }
   memset(c->zero16, 0, sizeof(c->zero16));
   // column forms for the units kernel: A^(128 k) and A^e, e = -127 .. 1
   {
@@ -136,10 +144,8 @@ void build_consts(DevConsts* c) {
       memcpy(c->shift_cols[k], m.col, sizeof(m.col));
       m = gf2::mul(row, m);
     }
-    for (uint32_t i = 0; i < kFinCols; i++) {
-      const gf2::Mat f = gf2::byte_pow((int64_t)i - 127);
-      memcpy(c->fin_cols[i], f.col, sizeof(f.col));
-    }
+    gf2::Mat f = gf2::byte_pow(-127);
+    for (uint32_t i = 0; i < kFinCols; i++, f = gf2::mul(fwd1, f)) memcpy(c->fin_cols[i], f.col, sizeof(f.col));
   }
 }
 
