@@ -722,7 +722,9 @@ def test_db_check_gpu_matches_the_reference_on_a_db_bench_database(torch_cuda, t
     bytes flipped in data blocks of three tables and in the WAL, both list the
     SAME failing blocks (file:offset) and the same reporter calls and dropped
     bytes, with the tables mapped read-only (staged) and read into heap
-    buffers (page-locked in place).  Skipped where the reference binaries were
+    buffers (page-locked in place).  On the clean database, every table's
+    filter block is also rebuilt on the GPU from its keys (byte-identical) and
+    every key probed in it (no false negatives).  Skipped where the reference binaries were
     not built."""
     import os
     import shutil
@@ -737,11 +739,15 @@ def test_db_check_gpu_matches_the_reference_on_a_db_bench_database(torch_cuda, t
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     rc, v = db_verify(os.path.join(ref, "db_verify"), str(db))
-    g = db_check_gpu(str(db), "0", tmp_path)
+    g = db_check_gpu(str(db), "0", tmp_path, "--filters")
     print("clean", v, g)
     assert rc == 0 and v["bad_blocks"] == [] and g["bad_blocks"] == []
     assert (g["tables"], g["blocks"], g["records"]) == (v["tables"], v["blocks"], v["records"])
     assert g["log_corruptions"] == v["log_errors"] == 0
+    # every table's filter block rebuilt on the GPU from its own keys: byte-identical,
+    # and no key of the table is ever filtered out
+    assert g["filters_rebuilt"] == g["filters_identical"] == g["tables"] and g["filter_tables_skipped"] == 0, g
+    assert g["keys_probed"] == v["entries"] and g["false_negatives"] == 0, g
     # corrupt a copy: one byte in the data region of three finished tables
     # (inside some data block or its trailer), one in the middle of the WAL
     bad = tmp_path / "bad"

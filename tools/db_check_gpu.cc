@@ -2,7 +2,7 @@
 // every log, of an lsbm database directory checked on the GPU with the
 // library's C++ layers only (no reference code linked):
 //
-//   db_check_gpu DIR [device | --parse-only] [--read=heap]
+//   db_check_gpu DIR [device | --parse-only] [--read=heap] [--filters]
 //
 // Tables (*.ldb): each file mapped read-only (or, --read=heap, read into a
 // writable heap buffer), its footer and index block parsed (the footer of
@@ -15,7 +15,9 @@
 // page-locked for the call).  Logs (*.log, MANIFEST-*): lsbm::log::BatchReader,
 // one GPU batch per file, then the reference reader's records and Reporter
 // calls (common/log_reader.cc:59-162).  --parse-only: the blocks gathered and
-// counted, no device call.
+// counted, no device call.  --filters: also every table's filter block
+// rebuilt on the GPU from its keys and compared byte for byte, and every key
+// probed in it (no false negatives).
 //
 // One JSON line: the counts, every failing block as "file:offset", the
 // reporter's calls, and the time of each phase (host CPU too; the device's
@@ -41,6 +43,7 @@
 #include <vector>
 
 #include "lsbm_crc32c.h"
+#include "lsbm/filter_block.h"
 #include "lsbm/log_checksum.h"
 #include "lsbm/table_checksum.h"
 
@@ -81,23 +84,32 @@ bool handle(const char*& p, const char* end, lsbm::BlockHandle* h) {
   return varint(p, end, &h->offset) && varint(p, end, &h->size);
 }
 
-// The values of the entries of block [data, data + n) (contents only, no
-// trailer): prefix-compressed entries, then the restart array and its count.
-bool block_values(const char* data, size_t n, std::vector<std::string>* values) {
+// The entries of block [data, data + n) (contents only, no trailer):
+// prefix-compressed entries (key = the previous key's first `shared` bytes +
+// the entry's own), then the restart array and its count.  keys (optional)
+// receives the full keys, values the values.
+bool block_entries(const char* data, size_t n, std::vector<std::string>* keys, std::vector<std::string>* values) {
   if (n < 4) return false;
   const uint32_t restarts = le32(data + n - 4);
   if (restarts > (n - 4) / 4) return false;
   const char* p = data;
   const char* end = data + n - 4 - 4 * (size_t)restarts;
+  std::string key;
   while (p < end) {
     uint64_t shared, non_shared, value_len;
     if (!varint(p, end, &shared) || !varint(p, end, &non_shared) || !varint(p, end, &value_len)) return false;
-    if ((uint64_t)(end - p) < non_shared + value_len) return false;
+    if ((uint64_t)(end - p) < non_shared + value_len || shared > key.size()) return false;
+    key.resize(shared);
+    key.append(p, non_shared);
     p += non_shared;
-    values->emplace_back(p, value_len);
+    if (keys) keys->push_back(key);
+    if (values) values->emplace_back(p, value_len);
     p += value_len;
   }
   return true;
+}
+bool block_values(const char* data, size_t n, std::vector<std::string>* values) {
+  return block_entries(data, n, nullptr, values);
 }
 
 struct Table {
@@ -106,11 +118,14 @@ struct Table {
   char* bytes = nullptr;         // the image (heap, or a read-only mapping)
   size_t size = 0;
   bool mapped = false;
-  std::vector<lsbm::BlockHandle> handles;
+  std::vector<lsbm::BlockHandle> handles;  // index, data blocks, metaindex, meta blocks
+  size_t data_blocks = 0;                  // handles[1, 1 + data_blocks)
+  bool has_filter = false;
+  lsbm::BlockHandle filter = {0, 0};       // the "filter.<policy>" meta block
   Table() = default;
   Table(Table&& o) noexcept
       : name(std::move(o.name)), heap(std::move(o.heap)), bytes(o.bytes), size(o.size), mapped(o.mapped),
-        handles(std::move(o.handles)) {
+        handles(std::move(o.handles)), data_blocks(o.data_blocks), has_filter(o.has_filter), filter(o.filter) {
     o.bytes = nullptr;
     o.mapped = false;
   }
@@ -138,7 +153,7 @@ bool table_blocks(Table* t, std::string* why) {
     return inside(h) && t->bytes[h.offset + h.size] == lsbm::kNoCompression &&
            block_values(t->bytes + h.offset, h.size, v);
   };
-  std::vector<std::string> entries, metas;
+  std::vector<std::string> entries, meta_keys, metas;
   if (!values(index, &entries)) return *why = "index block", false;
   t->handles.push_back(index);
   for (const std::string& e : entries) {
@@ -147,13 +162,20 @@ bool table_blocks(Table* t, std::string* why) {
     if (!handle(q, e.data() + e.size(), &h)) return *why = "index entry", false;
     t->handles.push_back(h);
   }
-  if (!values(meta, &metas)) return *why = "metaindex block", false;
+  t->data_blocks = entries.size();
+  if (!inside(meta) || t->bytes[meta.offset + meta.size] != lsbm::kNoCompression ||
+      !block_entries(t->bytes + meta.offset, meta.size, &meta_keys, &metas))
+    return *why = "metaindex block", false;
   t->handles.push_back(meta);
-  for (const std::string& e : metas) {
-    const char* q = e.data();
+  for (size_t i = 0; i < metas.size(); i++) {
+    const char* q = metas[i].data();
     lsbm::BlockHandle h;
-    if (!handle(q, e.data() + e.size(), &h)) return *why = "metaindex entry", false;
+    if (!handle(q, metas[i].data() + metas[i].size(), &h)) return *why = "metaindex entry", false;
     t->handles.push_back(h);
+    if (meta_keys[i].compare(0, 7, "filter.") == 0 && inside(h)) {  // (table/table_builder.cc:280-284)
+      t->has_filter = true;
+      t->filter = h;
+    }
   }
   return true;
 }
@@ -221,13 +243,17 @@ std::string json_escape(const std::string& s) {
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: %s DIR [device | --parse-only] [--read=heap]\n", argv[0]);
+    fprintf(stderr, "usage: %s DIR [device | --parse-only] [--read=heap] [--filters]\n", argv[0]);
     return 2;
   }
   const std::string dir = argv[1];
   const bool parse_only = argc > 2 && strcmp(argv[2], "--parse-only") == 0;
   const int device = argc > 2 && !parse_only ? atoi(argv[2]) : 0;
-  const bool heap = argc > 3 && strcmp(argv[3], "--read=heap") == 0;
+  bool heap = false, filters = false;
+  for (int a = 3; a < argc; a++) {
+    heap = heap || strcmp(argv[a], "--read=heap") == 0;
+    filters = filters || strcmp(argv[a], "--filters") == 0;
+  }
   std::vector<std::string> tables, logs;
   if (DIR* d = opendir(dir.c_str())) {
     while (dirent* e = readdir(d)) {
@@ -340,6 +366,91 @@ int main(int argc, char** argv) {
   }
   const double t3 = now_ms(), c3 = cpu_ms();
 
+  // --filters: every table's filter block rebuilt on the GPU from the table's
+  // own keys, as its TableBuilder built it -- StartBlock(0), each data
+  // block's keys, then StartBlock(the offset after the block and its trailer)
+  // (table/table_builder.cc:79-81, 129-131, 143-157) -- one FinishFilterBlocks
+  // batch for all tables, compared byte for byte with the table's filter
+  // block; then every key looked up in it (FilterBlockReader::KeyMayMatch,
+  // table/filter_block.cc:78-109, one batch per table): a filter never says
+  // no to a key its table holds.  db_bench's policy: 20 bits per key over user
+  // keys (lsbm/db_bench.cc:100, InternalFilterPolicy, lsbm/db_impl.cc:110).
+  size_t filters_rebuilt = 0, filters_identical = 0, filter_tables_skipped = 0;
+  uint64_t keys_probed = 0, false_negatives = 0;
+  double filters_build_ms = 0, filters_probe_ms = 0;
+  if (filters && !parse_only) {
+    const lsbm::BloomOptions bo;  // (bits_per_key 20, internal keys)
+    std::vector<std::unique_ptr<lsbm::FilterBlockBuilder>> builders;
+    std::vector<lsbm::FilterBlockBuilder*> ptrs;
+    std::vector<const Table*> of;
+    struct Probe {
+      std::vector<uint64_t> block_offsets, key_offsets{0};
+      std::string keys;
+    };
+    std::vector<Probe> probes;
+    const double f0 = now_ms();
+    for (const Table& t : ts) {
+      if (!t.has_filter) continue;
+      bool plain = true;
+      for (size_t i = 1; i <= t.data_blocks && plain; i++)
+        plain = t.bytes[t.handles[i].offset + t.handles[i].size] == lsbm::kNoCompression;
+      if (!plain) {
+        filter_tables_skipped++;  // (a snappy data block would need decoding first)
+        continue;
+      }
+      builders.emplace_back(new lsbm::FilterBlockBuilder(bo));
+      lsbm::FilterBlockBuilder* fb = builders.back().get();
+      Probe pr;
+      fb->StartBlock(0);
+      std::vector<std::string> keys;
+      for (size_t i = 1; i <= t.data_blocks; i++) {
+        const lsbm::BlockHandle& h = t.handles[i];
+        keys.clear();
+        if (!block_entries(t.bytes + h.offset, h.size, &keys, nullptr)) {
+          fprintf(stderr, "%s: data block at %llu does not parse\n", t.name.c_str(), (unsigned long long)h.offset);
+          return 1;
+        }
+        for (const std::string& k : keys) {
+          fb->AddKey(k.data(), k.size());
+          pr.keys += k;
+          pr.key_offsets.push_back(pr.keys.size());
+          pr.block_offsets.push_back(h.offset);
+        }
+        fb->StartBlock(h.offset + h.size + lsbm::kBlockTrailerSize);
+      }
+      ptrs.push_back(fb);
+      of.push_back(&t);
+      probes.push_back(std::move(pr));
+    }
+    std::vector<std::string> rebuilt(ptrs.size());
+    const lsbm::Status fs = lsbm::FinishFilterBlocks(device, ptrs.data(), ptrs.size(), rebuilt.data());
+    filters_build_ms = now_ms() - f0;
+    if (!fs.ok()) {
+      fprintf(stderr, "FinishFilterBlocks: %s\n", fs.ToString().c_str());
+      return 1;
+    }
+    const double p0 = now_ms();
+    for (size_t j = 0; j < of.size(); j++) {
+      const Table& t = *of[j];
+      filters_rebuilt++;
+      const char* own = t.bytes + t.filter.offset;
+      filters_identical += rebuilt[j].size() == t.filter.size && memcmp(rebuilt[j].data(), own, t.filter.size) == 0;
+      lsbm::FilterBlockReader rd(bo, own, t.filter.size);
+      std::vector<uint8_t> may;
+      const Probe& pr = probes[j];
+      const size_t nk = pr.block_offsets.size();
+      const lsbm::Status ps = rd.KeyMayMatch(device, pr.block_offsets.data(), pr.keys.data(), pr.key_offsets.data(),
+                                             nk, &may);
+      if (!ps.ok()) {
+        fprintf(stderr, "KeyMayMatch: %s\n", ps.ToString().c_str());
+        return 1;
+      }
+      keys_probed += nk;
+      for (size_t i = 0; i < nk; i++) false_negatives += may[i] == 0;
+    }
+    filters_probe_ms = now_ms() - p0;
+  }
+
   printf("{\"tables\": %zu, \"unfinished\": %zu, \"blocks\": %llu, \"table_bytes\": %llu, \"bad_blocks\": [",
          ts.size(), unfinished.size(), (unsigned long long)blocks, (unsigned long long)bytes);
   for (size_t i = 0; i < bad.size(); i++) printf("%s\"%s\"", i ? ", " : "", json_escape(bad[i]).c_str());
@@ -352,6 +463,12 @@ int main(int argc, char** argv) {
          (unsigned long long)rep.bytes, t0 - ti, t1 - t0, t2 - t1, again_ms, t3 - t2b, t3 - t0 - again_ms,
          c3 - c0 - again_cpu_ms, nthreads);
   for (size_t i = 0; i < unfinished.size(); i++) printf("%s\"%s\"", i ? ", " : "", json_escape(unfinished[i]).c_str());
-  printf("]}\n");
+  printf("]");
+  if (filters)
+    printf(", \"filters_rebuilt\": %zu, \"filters_identical\": %zu, \"filter_tables_skipped\": %zu, "
+           "\"keys_probed\": %llu, \"false_negatives\": %llu, \"filters_build_ms\": %.3f, \"filters_probe_ms\": %.3f",
+           filters_rebuilt, filters_identical, filter_tables_skipped, (unsigned long long)keys_probed,
+           (unsigned long long)false_negatives, filters_build_ms, filters_probe_ms);
+  printf("}\n");
   return 0;
 }
