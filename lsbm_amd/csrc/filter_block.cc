@@ -11,6 +11,8 @@
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 
+#include <memory>
+
 #include "../../include/lsbm_bloom.h"
 #include "host_session.h"
 
@@ -54,23 +56,42 @@ Status FilterBlockBuilder::Finish(int device, std::string* result) {
 Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_t n,
                           std::string* results) {
   if (n == 0) return Status::OK();
+  HostTiming tm("FinishFilterBlocks");  // (LSBM_HOST_TIMING=1: prep = layout, copy = uploads,
+                                        //  enqueue = build, wait = download, post = blocks)
+  double ph = HostTiming::now();
+  auto lap = [&](HostTiming::Phase p) {
+    const double t = HostTiming::now();
+    tm.add(p, t - ph);
+    ph = t;
+  };
   const int bpk = builders[0]->options_.bits_per_key;
   const bool internal = builders[0]->options_.internal_keys;
   if (bpk < 0) return Status::InvalidArgument("bits_per_key < 0");
-  // host layout of every block
-  std::string keys;
-  std::vector<uint64_t> key_offs, first, out_off;
-  std::vector<uint64_t> data_base(n), data_size(n);
-  std::vector<std::vector<uint32_t>> offsets(n);
-  uint64_t out_total = 0;
+  // host layout of every block.  The builders' keys are not concatenated on
+  // the host: each builder's key bytes go to their place in the device
+  // buffer as they are, and only the key offsets are rebased here (into a
+  // vector sized once).  (Concatenating 240 MB of keys for a 10M-key
+  // compaction cost more than the rest of the call.)
+  uint64_t total_keys = 0, total_bytes = 0;
   for (size_t t = 0; t < n; t++) {
     FilterBlockBuilder& b = *builders[t];
     if (b.options_.bits_per_key != bpk || b.options_.internal_keys != internal)
       return Status::InvalidArgument("one bits_per_key and key kind per batch");
     if (b.pending_ < b.starts_.size()) b.GenerateFilter();  // Finish, :37-39
-    const uint64_t key_base = key_offs.size(), byte_base = keys.size();
-    for (uint64_t s : b.starts_) key_offs.push_back(byte_base + s);
-    keys += b.keys_;
+    total_keys += b.starts_.size();
+    total_bytes += b.keys_.size();
+  }
+  std::vector<uint64_t> key_offs, first, out_off, byte_base(n);
+  key_offs.reserve(total_keys + 1);
+  std::vector<uint64_t> data_base(n), data_size(n);
+  std::vector<std::vector<uint32_t>> offsets(n);
+  uint64_t out_total = 0, bytes_so_far = 0;
+  for (size_t t = 0; t < n; t++) {
+    FilterBlockBuilder& b = *builders[t];
+    const uint64_t key_base = key_offs.size();
+    byte_base[t] = bytes_so_far;
+    for (uint64_t s : b.starts_) key_offs.push_back(bytes_so_far + s);
+    bytes_so_far += b.keys_.size();
     uint64_t size = 0;
     for (const auto& r : b.filters_) {
       offsets[t].push_back((uint32_t)size);  // filter_offsets_ (:56, :70)
@@ -84,40 +105,47 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
     data_size[t] = size;
     out_total += size;
   }
-  key_offs.push_back(keys.size());
+  key_offs.push_back(total_bytes);
   first.push_back(key_offs.size() - 1);  // filters cover every key, in order
-  std::vector<char> data(out_total);
+  std::unique_ptr<char[]> data(new char[out_total ? out_total : 1]);
   const size_t nf = out_off.size();
+  lap(HostTiming::kPrep);
   if (nf) {  // one launch on the device's session (host_session.h)
     SessionLease ss;
     Status s = ss.Open(device);
     if (!s.ok()) return s;
     void *d_keys, *d_offs, *d_first, *d_out_off, *d_out;
-    hipError_t e = ss->scratch(0, keys.size(), &d_keys);
+    hipError_t e = ss->scratch(0, total_bytes ? total_bytes : 1, &d_keys);
     if (e == hipSuccess) e = ss->scratch(1, key_offs.size() * sizeof(uint64_t), &d_offs);
     if (e == hipSuccess) e = ss->scratch(2, first.size() * sizeof(uint64_t), &d_first);
     if (e == hipSuccess) e = ss->scratch(3, out_off.size() * sizeof(uint64_t), &d_out_off);
     if (e == hipSuccess) e = ss->scratch(4, out_total, &d_out);
-    if (e == hipSuccess) e = ss->upload(d_keys, keys.data(), keys.size());
+    for (size_t t = 0; t < n && e == hipSuccess; t++)
+      e = ss->upload(static_cast<char*>(d_keys) + byte_base[t], builders[t]->keys_.data(), builders[t]->keys_.size());
     if (e == hipSuccess) e = ss->upload(d_offs, key_offs.data(), key_offs.size() * sizeof(uint64_t));
     if (e == hipSuccess) e = ss->upload(d_first, first.data(), first.size() * sizeof(uint64_t));
     if (e == hipSuccess) e = ss->upload(d_out_off, out_off.data(), out_off.size() * sizeof(uint64_t));
     if (e != hipSuccess) return hip_status(e, "staging");
+    lap(HostTiming::kCopy);
     if (lsbm_bloom_build_dev(static_cast<const uint8_t*>(d_keys), static_cast<const uint64_t*>(d_offs),
                              internal ? LSBM_INTERNAL_KEY_SUFFIX : 0,
                              static_cast<const uint64_t*>(d_first), static_cast<const uint64_t*>(d_out_off),
                              nf, bpk, static_cast<uint8_t*>(d_out), ss->stream()) != LSBM_OK)
       return Status::IOError(lsbm_crc32c_last_error());
-    e = ss->download(data.data(), d_out, out_total);
+    lap(HostTiming::kEnqueue);
+    e = ss->download(data.get(), d_out, out_total);
     if (e != hipSuccess) return hip_status(e, "filters");
+    lap(HostTiming::kWait);
   }
   for (size_t t = 0; t < n; t++) {  // :41-49
     std::string& r = results[t];
-    r.assign(data.data() + data_base[t], data_size[t]);
+    r.reserve(data_size[t] + 4 * offsets[t].size() + 5);
+    r.assign(data.get() + data_base[t], data_size[t]);
     for (uint32_t o : offsets[t]) put_fixed32(&r, o);
     put_fixed32(&r, (uint32_t)data_size[t]);
     r.push_back((char)LSBM_FILTER_BASE_LG);
   }
+  lap(HostTiming::kPost);
   return Status::OK();
 }
 

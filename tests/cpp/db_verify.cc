@@ -4,7 +4,7 @@
 // oracle/Makefile `dbbench_gpu` as oracle/_ref/db_verify).  TEST
 // INFRASTRUCTURE.
 //
-//   db_verify DIR [--open]
+//   db_verify DIR [--open] [--filters]
 //
 // Per table file (*.ldb): the footer, then EVERY block read through
 // the reference's ReadBlock with verify_checksums (table/format.cc:66-103) --
@@ -15,24 +15,31 @@
 // and reported corruptions counted.  With --open (on a copy: recovery writes),
 // the database is opened by the reference's DB::Open with paranoid_checks and
 // iterated with verify_checksums; the count of live entries and an FNV-1a
-// digest over (key, value) pairs in order identify its content.  One JSON line.
+// digest over (key, value) pairs in order identify its content.  With
+// --filters, every table's filter block is rebuilt by the reference's own
+// FilterBlockBuilder from the table's keys (timed) and compared with its own.
+// One JSON line.
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <set>
 #include <string>
 #include <vector>
 
+#include "common/dbformat.h"
 #include "common/filename.h"
 #include "common/log_reader.h"
 #include "leveldb/comparator.h"
 #include "leveldb/db.h"
 #include "leveldb/env.h"
+#include "leveldb/filter_policy.h"
 #include "leveldb/iterator.h"
 #include "leveldb/options.h"
 #include "lsbm/version_edit.h"
 #include "table/block.h"
+#include "table/filter_block.h"
 #include "table/format.h"
 
 using namespace leveldb;
@@ -51,7 +58,7 @@ struct Counts {
 // One block's entries (values kept when asked for, counted into `entries`),
 // read through ReadBlock with or without verify_checksums.
 Status ReadEntries(RandomAccessFile* f, const BlockHandle& h, bool verify, std::vector<std::string>* values,
-                   uint64_t* entries) {
+                   uint64_t* entries, std::vector<std::string>* keys = nullptr) {
   ReadOptions ro;
   ro.verify_checksums = verify;
   BlockContents c;
@@ -61,12 +68,22 @@ Status ReadEntries(RandomAccessFile* f, const BlockHandle& h, bool verify, std::
   Iterator* it = b.NewIterator(BytewiseComparator());
   for (it->SeekToFirst(); it->Valid(); it->Next()) {
     if (values) values->push_back(it->value().ToString());
+    if (keys) keys->push_back(it->key().ToString());
     if (entries) ++*entries;
   }
   s = it->status();
   delete it;
   return s;
 }
+
+// --filters: one table's data blocks' keys and its filter block, read ahead
+// of the timed rebuild
+struct FilterJob {
+  std::string name;
+  std::vector<std::vector<std::string>> block_keys;
+  std::vector<uint64_t> next_offsets;  // after each data block and its trailer
+  std::string filter;                  // the table's own filter block
+};
 
 // listed: whether any MANIFEST edit added this table.  db_bench exits without
 // waiting for its background work, so tables being written at that moment
@@ -80,7 +97,7 @@ Status ReadEntries(RandomAccessFile* f, const BlockHandle& h, bool verify, std::
 // mismatch is listed in `bad` as "file:offset" and the walk goes on (the
 // index and metaindex are parsed unverified, as Table::Open reads them).
 void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool listed, Counts* n,
-                 std::vector<std::string>* bad) {
+                 std::vector<std::string>* bad, std::vector<FilterJob>* jobs) {
   const std::string path = dir + "/" + name;
   uint64_t size = 0;
   RandomAccessFile* f = nullptr;
@@ -110,7 +127,9 @@ void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool
     s = v;
     return false;
   };
-  std::vector<std::string> index, meta;
+  std::vector<std::string> index, meta, meta_keys;
+  FilterJob job;
+  job.name = name;
   if (s.ok()) s = ReadEntries(f, footer.index_handle(), false, &index, nullptr);
   if (s.ok() && check(footer.index_handle(), nullptr, nullptr)) {
     for (size_t i = 0; s.ok() && i < index.size(); i++) {
@@ -118,9 +137,14 @@ void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool
       BlockHandle h;
       s = h.DecodeFrom(&v);
       if (s.ok()) check(h, nullptr, &n->entries);
+      if (s.ok() && jobs) {
+        job.block_keys.emplace_back();
+        s = ReadEntries(f, h, false, nullptr, nullptr, &job.block_keys.back());
+        job.next_offsets.push_back(h.offset() + h.size() + kBlockTrailerSize);
+      }
     }
   }
-  if (s.ok()) s = ReadEntries(f, footer.metaindex_handle(), false, &meta, nullptr);
+  if (s.ok()) s = ReadEntries(f, footer.metaindex_handle(), false, &meta, nullptr, &meta_keys);
   if (s.ok() && check(footer.metaindex_handle(), nullptr, nullptr)) {
     for (size_t i = 0; s.ok() && i < meta.size(); i++) {  // the filter block(s): raw bytes, verified
       Slice v(meta[i]);
@@ -133,6 +157,7 @@ void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool
       Status r = ReadBlock(f, ro, h, &c);
       n->blocks++;
       if (r.ok()) {
+        if (jobs && meta_keys[i].compare(0, 7, "filter.") == 0) job.filter.assign(c.data.data(), c.data.size());
         if (c.heap_allocated) delete[] c.data.data();
       } else if (r.ToString().find("block checksum mismatch") != std::string::npos) {
         bad->push_back(name + ":" + std::to_string(h.offset()));
@@ -144,6 +169,8 @@ void VerifyTable(Env* env, const std::string& dir, const std::string& name, bool
   if (!s.ok()) {
     n->table_errors++;
     n->error(path, s);
+  } else if (jobs && !job.filter.empty()) {
+    jobs->push_back(std::move(job));
   }
   delete f;
 }
@@ -185,7 +212,12 @@ int main(int argc, char** argv) {
     return 2;
   }
   const std::string dir = argv[1];
-  const bool open = argc > 2 && strcmp(argv[2], "--open") == 0;
+  bool open = false, filters = false;
+  for (int a = 2; a < argc; a++) {
+    open = open || strcmp(argv[a], "--open") == 0;
+    filters = filters || strcmp(argv[a], "--filters") == 0;
+  }
+  std::vector<FilterJob> jobs;
   Env* env = Env::Default();
   std::vector<std::string> files;
   Status s = env->GetChildren(dir, &files);
@@ -225,9 +257,35 @@ int main(int argc, char** argv) {
     if (!ParseFileName(files[i], &number, &type)) continue;
     const std::string path = dir + "/" + files[i];
     if (type == kTableFile)
-      VerifyTable(env, dir, files[i], listed.count(number) != 0, &n, &bad);
+      VerifyTable(env, dir, files[i], listed.count(number) != 0, &n, &bad, filters ? &jobs : nullptr);
     else if (type == kLogFile || type == kDescriptorFile)
       VerifyLog(env, path, &n);
+  }
+  // --filters: every table's filter block rebuilt by the reference's own
+  // FilterBlockBuilder from the table's keys, fed as TableBuilder feeds it
+  // (StartBlock(0), AddKey per key, StartBlock after each data block) with
+  // db_bench's policy (InternalFilterPolicy over NewBloomFilterPolicy(20),
+  // lsbm/db_bench.cc:100, lsbm/db_impl.cc:110), timed, and compared with the
+  // table's own block
+  size_t filters_identical = 0;
+  double filters_ms = 0;
+  if (filters) {
+    const FilterPolicy* bloom = NewBloomFilterPolicy(20);
+    InternalFilterPolicy ifp(bloom);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::string> rebuilt;
+    for (const FilterJob& j : jobs) {
+      FilterBlockBuilder fb(&ifp);
+      fb.StartBlock(0);
+      for (size_t b = 0; b < j.block_keys.size(); b++) {
+        for (const std::string& k : j.block_keys[b]) fb.AddKey(k);
+        fb.StartBlock(j.next_offsets[b]);
+      }
+      rebuilt.push_back(fb.Finish().ToString());
+    }
+    filters_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (size_t i = 0; i < jobs.size(); i++) filters_identical += rebuilt[i] == jobs[i].filter;
+    delete bloom;
   }
   uint64_t live = 0, digest = 1469598103934665603ull;  // FNV-1a 64
   std::string open_error;
@@ -262,6 +320,9 @@ int main(int argc, char** argv) {
          (unsigned long long)n.tables, (unsigned long long)n.unfinished, (unsigned long long)n.blocks, (unsigned long long)n.entries,
          (unsigned long long)n.table_errors, (unsigned long long)n.logs, (unsigned long long)n.records,
          (unsigned long long)n.log_errors, (unsigned long long)n.dropped_bytes, n.first_error.c_str());
+  if (filters)
+    printf(", \"filters_rebuilt\": %zu, \"filters_identical\": %zu, \"filters_ms\": %.3f", jobs.size(),
+           filters_identical, filters_ms);
   printf(", \"bad_blocks\": [");
   for (size_t i = 0; i < bad.size(); i++) printf("%s\"%s\"", i ? ", " : "", bad[i].c_str());
   printf("]");

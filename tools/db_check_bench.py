@@ -78,12 +78,19 @@ def main():
                          "verify_tables_again_GBps": round(g["table_bytes"] / (g["verify_tables_again_ms"] * 1e-3) / 1e9,
                                                            1)})
             print(json.dumps(rows[-1]), flush=True)
-    # and once with every table's filter block rebuilt and probed on the GPU
+    # and once with every table's filter block rebuilt: by the reference's own
+    # FilterBlockBuilder on one core, and on the GPU (then every key probed)
+    rc, wall, cpu, v = timed([os.path.join(REF, "db_verify"), db, "--filters"])
+    assert rc == 0 and v["filters_identical"] == v["filters_rebuilt"], v
+    rows.append({"tool": "reference db_verify --filters", "filters_rebuilt": v["filters_rebuilt"],
+                 "filters_identical": v["filters_identical"], "filters_ms": v["filters_ms"]})
+    print(json.dumps(rows[-1]), flush=True)
     rc, wall, cpu, g = timed([exe, db, "0", "--filters"])
     assert rc == 0 and g["filters_identical"] == g["filters_rebuilt"] == g["tables"] and g["false_negatives"] == 0, g
     rows.append({"tool": "db_check_gpu --filters", "filters_rebuilt": g["filters_rebuilt"],
                  "filters_identical": g["filters_identical"], "keys_probed": g["keys_probed"],
                  "false_negatives": g["false_negatives"], "filters_build_ms": g["filters_build_ms"],
+                 "filters_feed_ms": g["filters_feed_ms"], "filters_finish_ms": g["filters_finish_ms"],
                  "filters_probe_ms": g["filters_probe_ms"]})
     print(json.dumps(rows[-1]), flush=True)
     ref = [r for r in rows if r["tool"] == "reference db_verify"]
