@@ -68,10 +68,10 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
   const bool internal = builders[0]->options_.internal_keys;
   if (bpk < 0) return Status::InvalidArgument("bits_per_key < 0");
   // host layout of every block.  The builders' keys are not concatenated on
-  // the host: each builder's key bytes go to their place in the device
-  // buffer as they are, and only the key offsets are rebased here (into a
-  // vector sized once).  (Concatenating 240 MB of keys for a 10M-key
-  // compaction cost more than the rest of the call.)
+  // the host: they are gathered straight into the staging chunks on their way
+  // to the device, and only the key offsets are rebased here (into a vector
+  // sized once, builder by builder on the pool).  (Concatenating 240 MB of
+  // keys for a 10M-key compaction cost more than the rest of the call.)
   uint64_t total_keys = 0, total_bytes = 0;
   for (size_t t = 0; t < n; t++) {
     FilterBlockBuilder& b = *builders[t];
@@ -81,22 +81,32 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
     total_keys += b.starts_.size();
     total_bytes += b.keys_.size();
   }
-  std::vector<uint64_t> key_offs, first, out_off, byte_base(n);
-  key_offs.reserve(total_keys + 1);
+  // (no zero fill: every entry is written, in parallel, by the pass below)
+  std::unique_ptr<uint64_t[]> key_offs(new uint64_t[total_keys + 1]);
+  std::vector<uint64_t> first, out_off, byte_base(n), key_base(n);
   std::vector<uint64_t> data_base(n), data_size(n);
   std::vector<std::vector<uint32_t>> offsets(n);
-  uint64_t out_total = 0, bytes_so_far = 0;
+  uint64_t out_total = 0, bytes_so_far = 0, keys_so_far = 0;
+  for (size_t t = 0; t < n; t++) {
+    byte_base[t] = bytes_so_far;
+    key_base[t] = keys_so_far;
+    bytes_so_far += builders[t]->keys_.size();
+    keys_so_far += builders[t]->starts_.size();
+  }
+  // the rebased key offsets, builder by builder on the worker pool
+  parallel_for(n, [&](size_t t) {
+    const std::vector<uint64_t>& st = builders[t]->starts_;
+    uint64_t* o = key_offs.get() + key_base[t];
+    for (size_t k = 0; k < st.size(); k++) o[k] = byte_base[t] + st[k];
+  });
   for (size_t t = 0; t < n; t++) {
     FilterBlockBuilder& b = *builders[t];
-    const uint64_t key_base = key_offs.size();
-    byte_base[t] = bytes_so_far;
-    for (uint64_t s : b.starts_) key_offs.push_back(bytes_so_far + s);
-    bytes_so_far += b.keys_.size();
+    const uint64_t kb = key_base[t];
     uint64_t size = 0;
     for (const auto& r : b.filters_) {
       offsets[t].push_back((uint32_t)size);  // filter_offsets_ (:56, :70)
       if (r.hi > r.lo) {
-        first.push_back(key_base + r.lo);
+        first.push_back(kb + r.lo);
         out_off.push_back(out_total + size);
         size += lsbm_bloom_filter_bytes(r.hi - r.lo, bpk);
       }
@@ -105,8 +115,8 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
     data_size[t] = size;
     out_total += size;
   }
-  key_offs.push_back(total_bytes);
-  first.push_back(key_offs.size() - 1);  // filters cover every key, in order
+  key_offs[total_keys] = total_bytes;
+  first.push_back(total_keys);  // filters cover every key, in order
   std::unique_ptr<char[]> data(new char[out_total ? out_total : 1]);
   const size_t nf = out_off.size();
   lap(HostTiming::kPrep);
@@ -116,13 +126,14 @@ Status FinishFilterBlocks(int device, FilterBlockBuilder* const* builders, size_
     if (!s.ok()) return s;
     void *d_keys, *d_offs, *d_first, *d_out_off, *d_out;
     hipError_t e = ss->scratch(0, total_bytes ? total_bytes : 1, &d_keys);
-    if (e == hipSuccess) e = ss->scratch(1, key_offs.size() * sizeof(uint64_t), &d_offs);
+    if (e == hipSuccess) e = ss->scratch(1, (total_keys + 1) * sizeof(uint64_t), &d_offs);
     if (e == hipSuccess) e = ss->scratch(2, first.size() * sizeof(uint64_t), &d_first);
     if (e == hipSuccess) e = ss->scratch(3, out_off.size() * sizeof(uint64_t), &d_out_off);
     if (e == hipSuccess) e = ss->scratch(4, out_total, &d_out);
-    for (size_t t = 0; t < n && e == hipSuccess; t++)
-      e = ss->upload(static_cast<char*>(d_keys) + byte_base[t], builders[t]->keys_.data(), builders[t]->keys_.size());
-    if (e == hipSuccess) e = ss->upload(d_offs, key_offs.data(), key_offs.size() * sizeof(uint64_t));
+    std::vector<HostSession::Piece> pieces(n);  // every builder's keys, back to back: one gather
+    for (size_t t = 0; t < n; t++) pieces[t] = HostSession::Piece{builders[t]->keys_.data(), builders[t]->keys_.size()};
+    if (e == hipSuccess) e = ss->upload_pieces(d_keys, pieces.data(), n);
+    if (e == hipSuccess) e = ss->upload(d_offs, key_offs.get(), (total_keys + 1) * sizeof(uint64_t));
     if (e == hipSuccess) e = ss->upload(d_first, first.data(), first.size() * sizeof(uint64_t));
     if (e == hipSuccess) e = ss->upload(d_out_off, out_off.data(), out_off.size() * sizeof(uint64_t));
     if (e != hipSuccess) return hip_status(e, "staging");

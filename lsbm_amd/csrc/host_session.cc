@@ -808,24 +808,41 @@ hipError_t HostSession::wait(Stage& s) {
 
 hipError_t HostSession::upload(void* d, const void* h, size_t n) {
   if (n == 0) return hipSuccess;
-  Stage& s0 = stage_[0];
-  for (Stage& s : stage_) s.settled = false;
   if (host_pinned(h, n)) {
+    Stage& s0 = stage_[0];
+    for (Stage& s : stage_) s.settled = false;
     hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s0.stream);
     return e == hipSuccess ? hipStreamSynchronize(s0.stream) : e;
   }
+  const Piece one = {h, n};
+  return upload_pieces(d, &one, 1);
+}
+
+hipError_t HostSession::upload_pieces(void* d, const Piece* pieces, size_t count) {
+  size_t n = 0;
+  for (size_t p = 0; p < count; p++) n += pieces[p].n;
+  if (n == 0) return hipSuccess;
+  Stage& s0 = stage_[0];
+  for (Stage& s : stage_) s.settled = false;
   // through the stages' pinned buffers: stage i's copy overlaps stage i-1's
   // DMA (on the other stages' streams, so stage 0's queue is drained first)
   hipError_t e0 = hipStreamSynchronize(s0.stream);
   if (e0 != hipSuccess) return e0;
   int i = 0;
+  size_t p = 0, in_p = 0;  // the next byte to stage: piece p, offset in_p
   for (size_t off = 0; off < n; off += kChunkBytes, i = (i + 1) % kStages) {
     const size_t k = std::min(kChunkBytes, n - off);
     Stage& s = stage_[i];
     hipError_t e = wait(s);
     if (e == hipSuccess) e = s.bulk.reserve(kChunkBytes);
     if (e != hipSuccess) return e;
-    parallel_copy(s.bulk.h, static_cast<const char*>(h) + off, k);
+    for (size_t filled = 0; filled < k;) {  // the chunk from the pieces it spans
+      while (in_p == pieces[p].n) p++, in_p = 0;
+      const size_t take = std::min(k - filled, pieces[p].n - in_p);
+      parallel_copy(s.bulk.h + filled, static_cast<const char*>(pieces[p].h) + in_p, take);
+      filled += take;
+      in_p += take;
+    }
     e = hipMemcpyAsync(static_cast<char*>(d) + off, s.bulk.h, k, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return e;

@@ -128,6 +128,14 @@ class HostSession {
   // Synchronous: returns when the bytes have arrived.
   hipError_t upload(void* d, const void* h, size_t n);
   hipError_t download(void* h, const void* d, size_t n);
+  // upload of several host pieces laid back to back at d (a gather): the
+  // stages' chunks are filled from as many pieces as they span, one DMA per
+  // chunk, instead of one synchronous upload per piece.
+  struct Piece {
+    const void* h;
+    size_t n;
+  };
+  hipError_t upload_pieces(void* d, const Piece* pieces, size_t count);
 
   // Waits for a stage's enqueued work (no-op if idle); clears busy.  Sleeps
   // in short naps while the work is expected to take longer than ~60 us more
