@@ -6,8 +6,9 @@ Workload (BASELINE.json configs[1]): 1,048,576 blocks x
 The bytes: one dataset, block i = bytes [4096 i, 4096 (i + 1)) of the
 splitmix64 stream 0x5EED0000 (tests/golden/splitmix.py), generated on the
 device; rank r of N holds global blocks [r n, (r + 1) n).  One
-*step* = one lsbm_crc32c_fixed_dev launch over the whole batch (crc32c::Value
-of every block, util/crc32c.cc:286-329).
+*step* = one lsbm_crc32c_fixed_dev call over the whole batch (crc32c::Value
+of every block, util/crc32c.cc:286-329): one launch for the 1M-block config,
+back-to-back launches of 1M blocks for a 10M-block shard.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 

@@ -219,6 +219,16 @@ int current_device(DeviceState** out) {
   return ensure_device(dev, out);
 }
 
+// Blocks per launch of the fixed kernel for big batches
+// (LSBM_FIXED_SPLIT_BLOCKS; 0 = one launch whatever the size).
+uint64_t fixed_split_blocks() {
+  static const uint64_t b = [] {
+    const char* v = getenv("LSBM_FIXED_SPLIT_BLOCKS");
+    return v ? (uint64_t)strtoull(v, nullptr, 10) : (uint64_t)(1u << 20);
+  }();
+  return b;
+}
+
 int grid_for(const DeviceState* st, uint64_t n_blocks) {
   const uint64_t groups = (n_blocks + 7) / 8;
   const uint64_t wgs = (groups + kWavesPerWg - 1) / kWavesPerWg;
@@ -355,10 +365,18 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
   if (fast) {
     const gf2::Mat an = gf2::byte_pow((int64_t)len);
     const uint32_t k_value = gf2::apply(an, 0xffffffffu) ^ 0xffffffffu;
-    hipError_t e = launch_fixed(static_cast<const uint8_t*>(d_base), stride,
-                                (uint32_t)(len / kRowBytes), n_blocks, d_init, d_out, flags,
-                                k_value, st->d_consts, grid_for(st, n_blocks),
-                                static_cast<hipStream_t>(stream));
+    // A big batch goes as back-to-back launches of fixed_split_blocks() blocks
+    // on the caller's stream (one launch over a 10M-block
+    // shard ran 1-2 points under the same blocks a million at a time).
+    const uint64_t per = fixed_split_blocks();
+    hipError_t e = hipSuccess;
+    for (uint64_t f = 0; f < n_blocks && e == hipSuccess;) {
+      const uint64_t m = (per && n_blocks - f >= 2 * per) ? per : n_blocks - f;
+      e = launch_fixed(static_cast<const uint8_t*>(d_base) + f * stride, stride,
+                       (uint32_t)(len / kRowBytes), m, d_init ? d_init + f : nullptr, d_out + f, flags,
+                       k_value, st->d_consts, grid_for(st, m), static_cast<hipStream_t>(stream));
+      f += m;
+    }
     return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_fixed_kernel");
   }
   // Any other geometry: the ragged kernel with fixed-stride extents.

@@ -48,6 +48,24 @@ def test_fixed_fast_path(torch_cuda, oracle, length, stride, n, use_init, masked
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("use_init,masked", [(False, False), (True, True)])
+def test_fixed_batch_split_into_launches(torch_cuda, oracle, use_init, masked):
+    """A batch of >= 2 x LSBM_FIXED_SPLIT_BLOCKS (default 1M) blocks goes as
+    several launches (crc32c_engine.cc lsbm_crc32c_fixed_dev); every block,
+    the launch boundaries included, matches the oracle."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    length, n = 128, 3 * (1 << 20) + 77  # launches of 1M, 1M and 1M + 77 blocks
+    data = stream_bytes(4242, 0, n * length)
+    rng = np.random.default_rng(5)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if use_init else None
+    d = _dev(torch, data)
+    di = _dev(torch, init, torch.int32) if use_init else None
+    got = _u32(engine.crc32c_fixed(d, length, length, n, init=di, masked=masked))
+    want = oracle.batch_fixed(data, length, length, n, init, masked)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("length,stride,n,shift", [
     (4118, 4118, 64, 0), (4117, 4123, 31, 0), (1, 1, 100, 0), (0, 16, 5, 0), (100, 100, 77, 0),
     (4096, 4096, 20, 3), (4096, 4100, 20, 0), (70000, 70001, 5, 1), (3, 5, 1000, 0),

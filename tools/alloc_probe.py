@@ -2,11 +2,15 @@
 """The fixed kernel over one 10M-block (40 GiB) batch allocated three ways
 (per-GPU rate of a config-5 shard):
 
-    python tools/alloc_probe.py [--blocks 10000000]
+    LSBM_FIXED_SPLIT_BLOCKS=0 python tools/alloc_probe.py [--blocks 10000000]
+
+(=0: one launch per lsbm_crc32c_fixed_dev call, as the cases below assume;
+the library's default splits a batch of 2M+ blocks into 1M-block launches.)
 
   torch       torch.empty (the caching allocator's hipMalloc), as bench.py
   hipMalloc   hipMalloc directly
   contiguous  hipExtMallocWithFlags(..., hipDeviceMallocContiguous)
+  split       one torch buffer swept by launches of 512K-4M blocks
   chunks      the same blocks as 1M-block allocations, one launch each
 
 Each: fill (splitmix64 0x5EED0000), 0.3 s spin-up, then 20 launches between
@@ -84,6 +88,35 @@ def main():
             hip.hipFree(ctypes.c_void_p(ptr))
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+
+    # one torch buffer, swept by launches of `per` blocks each (back to back on
+    # the stream): whether the one-launch rate is the buffer or the launch
+    keep = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lb.lsbm_fill_splitmix64_dev(ctypes.c_void_p(keep.data_ptr()), nbytes, 0x5EED0000, sp) == 0
+    for per in (1 << 19, 1 << 20, 1 << 21, 1 << 22):
+        def launch_split():
+            for f in range(0, n, per):
+                m = min(per, n - f)
+                assert lb.lsbm_crc32c_fixed_dev(ctypes.c_void_p(keep.data_ptr() + f * L), L, L, m, None,
+                                                ctypes.c_void_p(out.data_ptr() + 4 * f), 0, sp) == 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.3:
+            launch_split()
+            torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(20):
+            launch_split()
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 20
+        same = bool(torch.equal(out.cpu(), ref)) if ref is not None else None
+        print(json.dumps({"alloc": "torch, one buffer, launches of %d blocks" % per, "blocks": n, "ms": round(ms, 4),
+                          "GiBps": round(n * L / (ms / 1e3) / 2**30, 1),
+                          "pct_8TBs": round(100 * n * L / (ms / 1e3) / 8e12, 2), "crcs_equal_torch": same}), flush=True)
+    del keep
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
     # the same blocks held as ten separate 1M-block allocations, one launch each
     chunks = []

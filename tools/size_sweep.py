@@ -2,7 +2,9 @@
 """The fixed kernel's rate against the batch's size and place (DESIGN.md section 6:
 per-GPU rate of a config-5 shard vs config 2):
 
-    python tools/size_sweep.py [--gib 40]
+    LSBM_FIXED_SPLIT_BLOCKS=0 python tools/size_sweep.py [--gib 40]
+
+(=0: one launch per call, as measured in round 5 before big batches were split.)
 
 One buffer of --gib GiB of 4 KiB blocks; lsbm_crc32c_fixed_dev over sub-batches
 of 1M, 2M, 4M and all blocks, at the buffer's start and end, each timed with HIP
