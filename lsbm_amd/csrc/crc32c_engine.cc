@@ -249,7 +249,7 @@ uint32_t u_noinit() {
 // lsbm_crc32c_init sets to keep freed memory).  Without that scratch, and
 // while the stream is being captured into a graph, the batch goes as one
 // range per wave.
-int run_ragged(RaggedArgs a, hipStream_t stream) {
+int run_ragged_one(RaggedArgs a, hipStream_t stream) {
   DeviceState* st = nullptr;
   int rc = current_device(&st);
   if (rc != LSBM_OK) return rc;
@@ -290,6 +290,30 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
   const hipError_t e = launch_ragged(a, (int)st->num_cus, stream);
   if (bounds) (void)hipFreeAsync(bounds, stream);
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_units_kernel");
+}
+
+// A big offsets batch (CRCs out) as back-to-back launches of
+// LSBM_RAGGED_SPLIT_BLOCKS blocks (0, the default: one launch; A/B, DESIGN.md
+// section 6 for the fixed-stride case).
+int run_ragged(RaggedArgs a, hipStream_t stream) {
+  static const uint64_t per = [] {
+    const char* v = getenv("LSBM_RAGGED_SPLIT_BLOCKS");
+    return v ? (uint64_t)strtoull(v, nullptr, 10) : (uint64_t)0;
+  }();
+  if (!(per && a.mode == kModeOut && a.extents == kExtOffsets && a.n >= 2 * per))
+    return run_ragged_one(a, stream);
+  for (uint64_t f = 0; f < a.n;) {
+    const uint64_t m = a.n - f >= 2 * per ? per : a.n - f;
+    RaggedArgs b = a;
+    b.offsets = a.offsets + f;
+    b.n = m;
+    b.out = a.out + f;
+    if (a.init) b.init = a.init + f;
+    const int rc = run_ragged_one(b, stream);
+    if (rc != LSBM_OK) return rc;
+    f += m;
+  }
+  return LSBM_OK;
 }
 
 }  // namespace
