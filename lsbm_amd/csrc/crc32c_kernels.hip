@@ -104,10 +104,27 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     loff = (blk < n_blocks ? g : 0u) * (uint32_t)stride + 16u * li;
     asm volatile("" : "+v"(loff));  // defined in every lane (see crc32c_units_kernel)
   };
-  // Static interleave: wave w takes groups w, w + nwaves, ...  At any moment
-  // the GPU streams one contiguous ~128 MiB window of the batch.  (A dynamic
-  // per-XCC work queue evened out per-wave finish times but was 5% slower
-  // end to end: DESIGN.md section 4.)
+  // Interleave: wave w starts at group w; a workgroup's k-th group is
+  // (k / 16) * nwaves + 16 * blockIdx + k % 16, so at any moment the GPU
+  // streams one contiguous window of the batch.  (A dynamic per-XCC work
+  // queue in global memory was 5% slower end to end: DESIGN.md section 4.)
+#ifndef LSBM_WG_STATIC
+  // A workgroup's groups are the static interleave's, but its waves take them
+  // in turn from an LDS counter, so a fast wave takes more of them: under the
+  // static split the waves' durations spread with an 18% CV and the first wave
+  // was done at 54% of the launch (tools/wave_spread.py);
+  // with the counter, 3.8% and 87%.  (-DLSBM_WG_STATIC: the static split, A/B.)
+  __shared__ uint32_t s_next;
+  if (threadIdx.x == 0) s_next = kWavesPerWg;  // (ordered by load_lds_tables' barrier)
+  auto next_grp = [&](uint64_t) -> uint64_t {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(&s_next, 1u);
+    k = __builtin_amdgcn_readfirstlane(k);
+    return (uint64_t)(k / kWavesPerWg) * nwaves + (uint64_t)blockIdx.x * kWavesPerWg + (k % kWavesPerWg);
+  };
+#else
+  auto next_grp = [&](uint64_t gp) -> uint64_t { return gp + nwaves; };
+#endif
   uint64_t grp = wave;
   DIAG_STAMP(0);
   if (grp < ngroups) {
@@ -119,7 +136,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
   DIAG_STAMP(1);
 
   bool first = true;
-  for (; grp < ngroups; grp += nwaves) {
+  for (; grp < ngroups; grp = next_grp(grp)) {
     const uint64_t blk = grp * 8 + g;
     const bool valid = blk < n_blocks;
     // Two banks of kPF rows: while one bank is absorbed the other's loads
