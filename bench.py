@@ -28,7 +28,10 @@ Extra fields: roofline (achieved algorithmic GB/s of the dominant kernel vs the
 at N=1 only, bounded sample), stream_read (the same buffer read with the CRC
 kernel's own access pattern and no CRC work: the measured read ceiling),
 host_staged (the same blocks checksummed from pinned host memory through
-lsbm_crc32c_batch_host: the PCIe-inclusive rate, rank 0 at N=1 only).
+lsbm_crc32c_batch_host: the PCIe-inclusive rate, rank 0 at N=1 only), ranks
+(per rank: its own elapsed time, bytes, GiB/s and kernel time per launch, its
+device's PCI address and NUMA node and its CPUs' NUMA nodes; the bytes add up
+to the aggregate).
 """
 import argparse
 import ctypes
@@ -131,6 +134,70 @@ def timed_steps(step, steps, warmup, sync, barrier, max_reduce, mark_start=None,
     barrier()
     sync()
     return max_reduce(time.perf_counter() - t0)
+
+
+def numa_node_of_cpus(cpus):
+    """The NUMA node(s) holding `cpus` (sysfs node cpulists), as a sorted list."""
+    nodes = set()
+    base = "/sys/devices/system/node"
+    try:
+        names = [d for d in os.listdir(base) if d.startswith("node") and d[4:].isdigit()]
+    except OSError:
+        return []
+    for d in names:
+        try:
+            with open(os.path.join(base, d, "cpulist")) as f:
+                text = f.read().strip()
+        except OSError:
+            continue
+        for part in filter(None, text.split(",")):
+            a, _, b = part.partition("-")
+            lo, hi = int(a), int(b or a)
+            if any(lo <= c <= hi for c in cpus):
+                nodes.add(int(d[4:]))
+                break
+    return sorted(nodes)
+
+
+def device_placement(torch, device):
+    """Where rank's GPU sits: its PCI address and that device's NUMA node
+    (sysfs), beside the NUMA node(s) of the CPUs this process may run on --
+    the first thing to look at when one rank of a node is slow."""
+    rec = {"device": device}
+    try:
+        p = torch.cuda.get_device_properties(device)
+        rec["name"] = p.name
+        dom, bus, dev = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        if bus is not None:
+            addr = f"{dom or 0:04x}:{bus:02x}:{dev or 0:02x}.0"
+            rec["pci"] = addr
+            try:
+                with open(f"/sys/bus/pci/devices/{addr}/numa_node") as f:
+                    rec["gpu_numa_node"] = int(f.read().strip())
+            except (OSError, ValueError):
+                rec["gpu_numa_node"] = None
+    except Exception as e:  # (a record, not a reason to fail the bench)
+        rec["error"] = str(e)
+    rec["cpu_numa_nodes"] = numa_node_of_cpus(os.sched_getaffinity(0))
+    return rec
+
+
+def rank_record(rank, elapsed_s, nbytes, kernel_ms_per_launch, placement):
+    """This rank's own line of the per-rank table (bench.py's JSON `ranks`)."""
+    return dict(rank=rank, elapsed_s=round(elapsed_s, 6), bytes=int(nbytes),
+                GiBps=round(nbytes / elapsed_s / 2**30, 2) if elapsed_s > 0 else None,
+                kernel_ms_per_launch=None if kernel_ms_per_launch is None else round(kernel_ms_per_launch, 4),
+                **placement)
+
+
+def gather_ranks(dist, world, rec):
+    """Every rank's record, in rank order, over the harness's process group
+    (gloo by default: CPU objects, no RCCL)."""
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return sorted(out, key=lambda r: r["rank"])
 
 
 def load_traffic(workload):
@@ -311,7 +378,10 @@ def main():
         if world > 1:
             dist.barrier()
 
+    mine = {}
+
     def max_reduce(x):
+        mine["elapsed_s"] = x  # (this rank's own time, for the per-rank table)
         t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -353,6 +423,11 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     stream_gbps = 10 * n * BLOCK / (e0.elapsed_time(e1) / 1e3) / 1e9
+
+    # per rank: its own elapsed time, bytes and rate, and where its GPU and
+    # CPUs sit (the aggregate `value` alone hides a slow rank)
+    ranks = gather_ranks(dist, world, rank_record(rank, mine["elapsed_s"], n * BLOCK * args.steps,
+                                                  kern_ms / args.steps, device_placement(torch, local)))
 
     total_bytes = n * BLOCK * world * args.steps
     value = total_bytes / t_max / 2**30
@@ -416,6 +491,7 @@ def main():
                             "crc_frac_of_stream_read": round(achieved / stream_gbps, 4)},
             "cpu_baseline": cpu,
             "host_staged": staged,
+            "ranks": ranks,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -45,23 +45,26 @@ std::vector<BlockHandle> LayoutBlocks(const std::vector<uint64_t>& sizes, uint64
 Status SealBlocks(int device, char* file, size_t file_size, const BlockHandle* handles,
                   const uint8_t* types, size_t n);
 
-// Batched ReadBlock verify.  ok (optional) receives one flag per block.
-// Returns Corruption("block checksum mismatch") if any block fails.
-//
-// The image's memory decides how it reaches the device:
-//  * `char*` -- writable memory the caller owns, as lsbm's ReadBlock has it:
-//    it preads every block into `new char[n + kBlockTrailerSize]`
+// How an image's memory may be page-locked for a call (VerifyBlocks,
+// VerifyTables; SealBlocks / SealTables write their images, so those are
+// writable by definition):
+//  * kImagesWritable -- writable memory the caller owns, as lsbm's ReadBlock
+//    has it: it preads every block into `new char[n + kBlockTrailerSize]`
 //    (table/format.cc:79-82; lsbm reads no table through mmap,
 //    util/env_posix.cc:329-330).  A small job's image is page-locked for the
 //    call and DMA-ed in place, as the seal's is (no staging copy);
-//  * `const char*` -- possibly a read-only mapping (an mmap'd table file),
+//  * kImagesReadOnly -- possibly a read-only mapping (an mmap'd table file),
 //    which must not be pinned for writing (that could copy a private
 //    mapping's pages out of the page cache): staged through pinned buffers
 //    unless the caller page-locked it.
+// The caller states it; it is never inferred from the pointer's constness.
+enum ImageMemory : uint8_t { kImagesReadOnly = 0, kImagesWritable = 1 };
+
+// Batched ReadBlock verify.  ok (optional) receives one flag per block.
+// Returns Corruption("block checksum mismatch") if any block fails, and
+// Corruption("truncated block read") for a handle past the image.
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
-                    size_t n, std::vector<uint8_t>* ok);
-Status VerifyBlocks(int device, char* file, size_t file_size, const BlockHandle* handles, size_t n,
-                    std::vector<uint8_t>* ok);
+                    size_t n, std::vector<uint8_t>* ok, ImageMemory memory = kImagesReadOnly);
 
 // One table file image in host memory: its blocks and, for sealing, their
 // CompressionType bytes.
@@ -81,9 +84,7 @@ struct TableImage {
 // the other.  A page-locked image (hipHostMalloc / hipHostRegister) is DMA-ed
 // in place; a pageable one is copied into pinned staging first.
 // VerifyTables' images are read-only memory unless `memory` says they are
-// writable heap buffers (see VerifyBlocks); SealTables writes its images, so
-// they are writable by definition.
-enum ImageMemory : uint8_t { kImagesReadOnly = 0, kImagesWritable = 1 };
+// writable heap buffers (ImageMemory above).
 Status SealTables(int device, const TableImage* tables, size_t count);
 Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok);
 Status VerifyTables(int device, const TableImage* tables, size_t count, std::vector<uint8_t>* ok,

@@ -212,6 +212,19 @@ int lsbm_test_ragged_kernel(int which);
  * affinity mask capped by the cgroup CPU quota (LSBM_HOST_THREADS overrides);
  * starts the pool. */
 int lsbm_host_threads(void);
+
+/* Long-lived page-locking of a host buffer that is reused from call to call
+ * (an embedder's table-image pool, integration/image_pool.h), inside the
+ * library's own page-lock bookkeeping: the buffer's pages are reserved, so no
+ * call page-locks over them and no other range on one of them is DMA-ed in
+ * place (its owner may unregister at any time), while a range inside the
+ * registered bytes is.  Refused (-1, nothing done) when a page of the range
+ * belongs to a live call's lock or to another registration, when either end
+ * is registered already, or past LSBM_PINNED_MB of such registrations.  No
+ * reference counterpart: lsbm pins nothing (host-side plumbing). */
+int lsbm_host_register(const void* p, uint64_t n);
+int lsbm_host_unregister(const void* p); /* p as registered; 0 or -1 */
+unsigned long long lsbm_host_registered_bytes(void);
 /* NUMA node of HIP device `device` (from its PCI bus id and
  * /sys/bus/pci/devices/<id>/numa_node), -1 if unknown. */
 int lsbm_device_numa_node(int device);

@@ -12,6 +12,10 @@
 // SealBlocks call (include/lsbm/table_checksum.h) fills every trailer --
 // data, filter, metaindex and index blocks -- on the GPU, the footer is
 // appended and the finished image goes to the WritableFile in one Append.
+// A seal the device cannot do (any non-OK SealBlocks status) is done on the
+// CPU with the library's scalar crc32c (integration/gpu_fallback.h): the
+// reference's checksum never fails, so neither does this builder's, and the
+// file is the same bytes either way.
 // The image is heap memory (std::string), so the call page-locks it for its
 // duration and DMAs it in place: ~0.36 ms per 16 MiB table on an MI355X
 // against ~8.7 ms of one core for the reference's per-block Extend loop
@@ -43,6 +47,7 @@
 #include "leveldb/env.h"
 #include "leveldb/filter_policy.h"
 #include "leveldb/options.h"
+#include "integration/gpu_fallback.h"
 #include "lsbm/table_checksum.h"
 #include "port/port.h"
 #include "table/block_builder.h"
@@ -61,9 +66,15 @@ class GpuTableBuilder {
   // so that a caller can hand the same buffer to table after table: its pages
   // are then faulted in once, and may stay page-locked (table_builder_gpu.cc);
   // null: a buffer of the builder's own.
+  // move / move_arg: the image-move observer (SetImageMoveObserver), in
+  // force from the constructor's own reserve on: a caller that page-locked
+  // `image` is told before any reallocation, this one included.
+  typedef void (*ImageMoveObserver)(void* arg);
   GpuTableBuilder(const Options& options, WritableFile* file, int device = 0, uint64_t size_hint = 0,
-                  std::string* image = nullptr)
+                  std::string* image = nullptr, ImageMoveObserver move = nullptr, void* move_arg = nullptr)
       : image_(image ? *image : own_image_),
+        move_observer_(move),
+        move_arg_(move_arg),
         options_(options),
         index_options_(options),
         file_(file),
@@ -75,7 +86,10 @@ class GpuTableBuilder {
     if (filter_) filter_->StartBlock(0);
     image_.clear();
     const size_t want = ImageBytesFor(size_hint);
-    if (want > image_.capacity()) image_.reserve(want);  // (never smaller: reserve may shrink)
+    if (want > image_.capacity()) {  // (never smaller: reserve may shrink)
+      if (move_observer_) move_observer_(move_arg_);
+      image_.reserve(want);
+    }
   }
   ~GpuTableBuilder() { delete filter_; }
 
@@ -125,7 +139,6 @@ class GpuTableBuilder {
 
   // Called before the image buffer reallocates (it is about to move): a
   // caller that page-locked the buffer unlocks it here.
-  typedef void (*ImageMoveObserver)(void* arg);
   void SetImageMoveObserver(ImageMoveObserver fn, void* arg) {
     move_observer_ = fn;
     move_arg_ = arg;
@@ -167,7 +180,19 @@ class GpuTableBuilder {
       seal_calls_++;
       const lsbm::Status s =
           lsbm::SealBlocks(device_, &image_[0], image_.size(), handles_.data(), types_.data(), handles_.size());
-      if (!s.ok()) status_ = Status::IOError("gpu seal", s.ToString());
+      if (!s.ok()) {
+        // The reference's checksum cannot fail (WriteRawBlock, table/
+        // table_builder.cc:243-250), and a failed compaction stops lsbm's
+        // writes (bg_error_, lsbm/db_impl.cc:567-573): a device that cannot
+        // seal (no device, a HIP error, no staging memory) costs the CPU
+        // trailers instead, the same bytes (integration/gpu_fallback.h).
+        // The handles are the builder's own, all inside the image, so the
+        // seal cannot have refused them.
+        SealTrailersOnHost(&image_[0], handles_.data(), types_.data(), handles_.size());
+        host_seals_++;
+        GpuFallbacks().seals.fetch_add(1, std::memory_order_relaxed);
+        last_gpu_error_ = s.ToString();
+      }
     }
     if (status_.ok()) {
       Footer footer;
@@ -187,6 +212,9 @@ class GpuTableBuilder {
   uint64_t NumEntries() const { return entries_; }
   uint64_t FileSize() const { return image_.size(); }  // (reserved trailers included, as the reference's offset)
   size_t SealCalls() const { return seal_calls_; }
+  // Finish calls whose seal fell back to the CPU, and the GPU's status then
+  size_t HostSeals() const { return host_seals_; }
+  const std::string& LastGpuError() const { return last_gpu_error_; }
   size_t Blocks() const { return handles_.size(); }
   // every block placed so far: data blocks, then filter, metaindex, index
   const std::vector<lsbm::BlockHandle>& Handles() const { return handles_; }
@@ -236,6 +264,8 @@ class GpuTableBuilder {
 
   std::string own_image_;
   std::string& image_;  // the table so far: blocks with reserved trailers
+  ImageMoveObserver move_observer_ = nullptr;
+  void* move_arg_ = nullptr;
   Options options_;
   Options index_options_;
   WritableFile* file_;
@@ -253,11 +283,11 @@ class GpuTableBuilder {
   std::vector<lsbm::BlockHandle> handles_;  // every block of the image, for the seal
   std::vector<uint8_t> types_;
   size_t seal_calls_ = 0;
+  size_t host_seals_ = 0;
+  std::string last_gpu_error_;
   bool closing_ = false;  // inside Finish
   DataBlockObserver observer_ = nullptr;
   void* observer_arg_ = nullptr;
-  ImageMoveObserver move_observer_ = nullptr;
-  void* move_arg_ = nullptr;
 
   GpuTableBuilder(const GpuTableBuilder&);
   void operator=(const GpuTableBuilder&);

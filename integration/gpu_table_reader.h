@@ -22,7 +22,11 @@
 // "Corruption: truncated block read" for a handle past the file), and the
 // caller can fall back to the reference's own verified iteration, which then
 // reproduces its exact behaviour around the bad block (it skips the block and
-// keeps the first error, table/two_level_iterator.cc).
+// keeps the first error, table/two_level_iterator.cc).  A verify the device
+// cannot do (a status other than Corruption: no device, a HIP error, no
+// staging memory) is done on the CPU with the library's scalar crc32c
+// (integration/gpu_fallback.h), with the same statuses: a GPU problem never
+// fails the read.
 //
 // Tested against the reference's reader in tests/cpp/ref_table_builder_gpu.cc
 // (oracle/Makefile `gputable`, run on the GPU by tests/test_gpu_parity.py).
@@ -36,6 +40,7 @@
 #include <string>
 #include <vector>
 
+#include "integration/gpu_fallback.h"
 #include "integration/image_pool.h"
 #include "leveldb/env.h"
 #include "leveldb/iterator.h"
@@ -131,12 +136,18 @@ inline Status OpenVerifiedTable(const Options& options, uint64_t file_number, Ra
   // ONE check of every data block's trailer on the GPU (ReadBlock's
   // verify_checksums test, table/format.cc:95-103, for all of them at once)
   if (s.ok()) {
-    const lsbm::Status v = lsbm::VerifyBlocks(device, f->data(), size, handles.data(), handles.size(), nullptr);
-    if (!v.ok()) {
+    const lsbm::Status v = lsbm::VerifyBlocks(device, f->data(), size, handles.data(), handles.size(), nullptr,
+                                                lsbm::kImagesWritable);
+    if (v.IsCorruption()) {
       const std::string m = v.ToString();
       const std::string kC = "Corruption: ";
-      s = v.IsCorruption() ? Status::Corruption(m.substr(m.compare(0, kC.size(), kC) == 0 ? kC.size() : 0))
-                           : Status::IOError("gpu verify", m);
+      s = Status::Corruption(m.substr(m.compare(0, kC.size(), kC) == 0 ? kC.size() : 0));
+    } else if (!v.ok()) {
+      // the device could not check them (no device, a HIP error, no staging
+      // memory): ReadBlock's check on the CPU instead, same statuses
+      // (integration/gpu_fallback.h), so a GPU problem never fails a read
+      s = VerifyBlocksOnHost(f->data(), size, handles.data(), handles.size());
+      GpuFallbacks().verifies.fetch_add(1, std::memory_order_relaxed);
     }
   }
   if (s.ok()) s = Table::Open(options, file_number, f, size, table);

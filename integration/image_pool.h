@@ -9,13 +9,15 @@
 // Measured on lsbm's db_bench (10M writes, 340 tables): +1.5-2 s of host CPU
 // against the reference and its writer 20% slower, until the builder's images
 // were pooled.  A pooled image keeps its pages, and
-// (LSBM_TABLE_REGISTER, default on) stays registered with hipHostRegister at
-// its current address and capacity, so a seal or verify DMAs it in place with
-// no per-call lock (the library takes a registered range as page-locked).
-// Before the string can move (a table that outgrows it), the registration is
-// dropped (Moving) -- memory is never freed while registered.
+// (LSBM_TABLE_REGISTER, default on) stays page-locked at its current address
+// and capacity through lsbm_host_register -- the library's own bookkeeping,
+// so the registration never overlaps a page another thread's call has locked,
+// and counts against LSBM_PINNED_MB -- and a seal or verify DMAs it in place
+// with no per-call lock.  Before the string can move (a table that outgrows
+// it), the registration is dropped (Moving) -- memory is never freed while
+// registered.
 //
-// Header-only; needs the HIP runtime (hipHostRegister), as the library does.
+// Header-only; links against liblsbm_crc32c.so (include/lsbm_crc32c.h).
 #ifndef LSBM_INTEGRATION_IMAGE_POOL_H_
 #define LSBM_INTEGRATION_IMAGE_POOL_H_
 
@@ -25,7 +27,7 @@
 #include <string>
 #include <vector>
 
-#include <hip/hip_runtime_api.h>
+#include "lsbm_crc32c.h"
 
 namespace leveldb {
 
@@ -65,7 +67,7 @@ class ImagePool {
   // the GpuTableBuilder image-move observer (arg: the PooledImage).
   static void Moving(void* arg) {
     PooledImage* p = static_cast<PooledImage*>(arg);
-    if (p->registered) (void)hipHostUnregister(p->registered);
+    if (p->registered) (void)lsbm_host_unregister(p->registered);
     p->registered = nullptr;
     p->registered_bytes = 0;
   }
@@ -77,11 +79,13 @@ class ImagePool {
       const size_t n = p->bytes.capacity();
       if (p->registered != at || p->registered_bytes != n) {
         Moving(p);
-        if (hipHostRegister(at, n, hipHostRegisterDefault) == hipSuccess) {
+        // through the library, inside its page-lock bookkeeping: never over a
+        // page another thread's image holds locked for a call, never a page
+        // another image's in-place DMA relies on, and within LSBM_PINNED_MB
+        // (refused: the image stays pooled, page-locked per call instead)
+        if (lsbm_host_register(at, n) == 0) {
           p->registered = at;
           p->registered_bytes = n;
-        } else {
-          (void)hipGetLastError();
         }
       }
     }

@@ -73,9 +73,10 @@ std::atomic<uint64_t> g_first_finish_ns(0);
 
 void PrintStats() {
   fprintf(stderr,
-          "lsbm_table_stats: tables_sealed_on_gpu=%llu blocks=%llu bytes=%llu finish_ms_total=%.3f "
-          "finish_ms_max=%.3f first_finish_at_ms=%.3f\n",
-          (unsigned long long)g_tables.load(), (unsigned long long)g_blocks.load(),
+          "lsbm_table_stats: tables_sealed_on_gpu=%llu tables_sealed_on_cpu_after_gpu_error=%llu blocks=%llu "
+          "bytes=%llu finish_ms_total=%.3f finish_ms_max=%.3f first_finish_at_ms=%.3f\n",
+          (unsigned long long)g_tables.load(), (unsigned long long)GpuFallbacks().seals.load(),
+          (unsigned long long)g_blocks.load(),
           (unsigned long long)g_bytes.load(), g_finish_ns.load() * 1e-6, g_finish_max_ns.load() * 1e-6,
           g_first_finish_ns.load() * 1e-6);
 }
@@ -97,9 +98,8 @@ struct TableBuilder::Rep {
         file(f),
         hint(g_size_hint.load(std::memory_order_relaxed)),
         image(ImagePool::Default().Take(GpuTableBuilder::ImageBytesFor(hint))),
-        gpu(opt, f, TableDevice(), hint, &image->bytes) {
+        gpu(opt, f, TableDevice(), hint, &image->bytes, &ImagePool::Moving, image) {
     gpu.SetDataBlockObserver(&Rep::Observe, this);
-    gpu.SetImageMoveObserver(&ImagePool::Moving, image);
   }
   ~Rep() { ImagePool::Default().Give(image); }  // (pooled and kept page-locked: integration/image_pool.h)
 
@@ -198,7 +198,7 @@ Status TableBuilder::Finish() {
   const uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   const uint64_t n = rep_->gpu.FileSize();
   if (s.ok()) {
-    g_tables++;
+    if (rep_->gpu.HostSeals() == 0) g_tables++;  // (a CPU-sealed table is counted by GpuFallbacks)
     g_blocks += rep_->gpu.Blocks();
     g_bytes += n;
     g_finish_ns += ns;

@@ -54,6 +54,9 @@ SIGNATURES = {
     "lsbm_test_fail_host_pipeline": (_int, [_int]),
     "lsbm_test_ragged_kernel": (_int, [_int]),
     "lsbm_host_threads": (_int, []),
+    "lsbm_host_register": (_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "lsbm_host_unregister": (_int, [ctypes.c_void_p]),
+    "lsbm_host_registered_bytes": (ctypes.c_ulonglong, []),
     "lsbm_device_numa_node": (_int, [_int]),
     "lsbm_test_pci_numa_node": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "lsbm_test_parse_cpulist": (_int, [ctypes.c_char_p, _vp, _int]),

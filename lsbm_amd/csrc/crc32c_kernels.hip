@@ -24,15 +24,13 @@
 namespace lsbm {
 
 
-#ifdef LSBM_DIAG_STAMPS  // diagnostic builds only (tools/ablate.sh): per-wave timeline
-__device__ uint64_t g_stamps[4][65536];  // start, first-data, end, xcc id
+#ifdef LSBM_DIAG_STAMPS  // diagnostic builds only: per-wave timeline (crc32c_units.h)
 extern "C" __attribute__((visibility("default"))) int lsbm_diag_stamps(uint64_t* host, int n) {
+  (void)n;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(uint64_t) * 4 * 65536) == hipSuccess ? 0 : -1;
 }
-#define DIAG_STAMP(k) do { if (lane == 0) g_stamps[k][wave & 65535] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define DIAG_STAMP(k) do { } while (0)
 #endif
+#define DIAG_STAMP(k) DIAG_STAMP_W(k, wave)
 
 #ifndef LSBM_PF
 #define LSBM_PF 4
@@ -178,13 +176,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     }
   }
   DIAG_STAMP(2);
-#ifdef LSBM_DIAG_STAMPS
-  if (lane == 0) {
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-    g_stamps[3][wave & 65535] = xcc;
-  }
-#endif
+  DIAG_XCC_W(wave);
 }
 // ---------------------------------------------------------------------------
 // Ragged path (crc32c_units.h): the units kernel walks each wave's range of
@@ -255,7 +247,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   bool chunked;
   uint32_t pi, p_end;
   uint64_t b_lo, b_hi;
+  DIAG_STAMP(0);
   wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
+  DIAG_STAMP(1);
   units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
   if constexpr (kMode == kModeSstCrc && kExt == kExtHandles) {
     if (args.file != nullptr) {  // (SstCrc is never chunked: [b_lo, b_hi) is this wave's range)
@@ -272,6 +266,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       }
     }
   }
+  DIAG_STAMP(2);
+  DIAG_XCC_W(wave);
 }
 
 // ---------------------------------------------------------------------------

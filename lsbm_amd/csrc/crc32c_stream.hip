@@ -134,6 +134,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   bool chunked;
   uint32_t pi, p_end;
   uint64_t b_lo, b_hi;
+  DIAG_STAMP_W(0, wave);
   wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
   const uint32_t* __restrict__ bnd = args.bounds;
   if (chunked) {
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     b_hi = bnd[pi + 1];
   }
   load_lds_tables<kStreamThreads>(g_lds, dc);
+  DIAG_STAMP_W(1, wave);
   const uint64_t base = reinterpret_cast<uint64_t>(args.base);
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const char* lds_c = reinterpret_cast<const char*>(g_lds);
@@ -706,6 +708,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     }
   }
   if (lane == 0u && nbad && args.nbad) atomicAdd(args.nbad, nbad);
+  DIAG_STAMP_W(2, wave);
+  DIAG_XCC_W(wave);
 }
 
 // Which batches go this way: no per-block init (crc32c::Value semantics;
@@ -743,6 +747,14 @@ hipError_t launch_stream(const RaggedArgs& a, int grid, hipStream_t stream) {
 }
 
 }  // namespace lsbm
+
+#ifdef LSBM_DIAG_STAMPS
+// diagnostic builds only: the stream kernel's per-wave timeline (crc32c_units.h)
+extern "C" __attribute__((visibility("default"))) int lsbm_diag_stamps_stream(uint64_t* host, int n) {
+  (void)n;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lsbm::g_stamps), sizeof(uint64_t) * 4 * 65536) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef LSBM_STREAM_STATS
 // diagnostic builds only: read and clear the counters

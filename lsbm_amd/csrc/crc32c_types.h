@@ -67,7 +67,13 @@ constexpr uint32_t km_entry(uint32_t lo, uint32_t hi) {
 constexpr uint32_t kStreamR0 = kStreamHM + kStreamMasks * 16;  // R0[d] = A^-d(~0), d = 0..127
 constexpr uint32_t kLdsBytes = kStreamR0 + 128 * 4;
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
-static_assert(kLdsBytes % 16 == 0 && kLdsBytes <= 160u * 1024u, "one LDS image per CU");
+// Besides the image, a kernel's own __shared__ words: the fixed kernel's work
+// counter (s_next, crc32c_kernels.hip) -- and the ragged kernels' once they
+// take pieces from one.  Reserved here, so that a table added to the image
+// fails this assert rather than hipcc's LDS limit on some kernel.
+constexpr uint32_t kLdsKernelWords = 4;
+static_assert(kLdsBytes % 16 == 0 && kLdsBytes + 4u * kLdsKernelWords <= 160u * 1024u,
+              "one LDS image per CU, plus the kernels' work counters");
 static_assert(kStreamHM % 16 == 0, "ds_read_b128 of a mask");
 
 constexpr uint32_t kShiftCols = 512;  // unit shifts up to 511 rows (64 KiB frames) by columns

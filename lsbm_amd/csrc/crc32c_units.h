@@ -14,6 +14,29 @@ namespace lsbm {
 
 __shared__ uint32_t g_lds[kLdsWords];
 
+// Diagnostic builds only (-DLSBM_DIAG_STAMPS, tools/wave_spread.py): every
+// wave stamps its start (0), its first data (1) and its end (2) with
+// s_memrealtime (100 MHz), and its XCC (3).  One array per kernel source
+// (internal linkage), read by that source's lsbm_diag_stamps* export.
+#ifdef LSBM_DIAG_STAMPS
+static __device__ uint64_t g_stamps[4][65536];
+#define DIAG_STAMP_W(k, w)                                                          \
+  do {                                                                              \
+    if ((threadIdx.x & 63u) == 0) g_stamps[k][(w) & 65535] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define DIAG_XCC_W(w)                                                               \
+  do {                                                                              \
+    if ((threadIdx.x & 63u) == 0) {                                                 \
+      uint32_t xcc_;                                                                \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_));     \
+      g_stamps[3][(w) & 65535] = xcc_;                                              \
+    }                                                                               \
+  } while (0)
+#else
+#define DIAG_STAMP_W(k, w) do { } while (0)
+#define DIAG_XCC_W(w) do { } while (0)
+#endif
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Global-address-space pointer: addresses built from integers would otherwise
 // be generic (flat) loads, which count on lgkmcnt too and force full drains.

@@ -79,6 +79,8 @@ static bool pinned_range(const void* p, size_t n) {
 //   * a range on such a page never counts as page-locked either: its bytes
 //     may lie inside another call's registration, which that call drops when
 //     it returns, so an in-place DMA from them could outlive it.
+size_t host_register_budget();  // (LSBM_PINNED_MB, below)
+
 namespace {
 std::mutex g_lock_mu;
 std::map<uintptr_t, uintptr_t> g_locked;  // [first page, end page) of each live CallLocks range
@@ -96,20 +98,110 @@ uintptr_t page_lo(const void* p) { return reinterpret_cast<uintptr_t>(p) & ~(pag
 uintptr_t page_hi(const void* p, size_t n) {
   return (reinterpret_cast<uintptr_t>(p) + n + page_size() - 1) & ~(page_size() - 1);
 }
+// Long-lived registrations made through lsbm_host_register (an embedder's
+// buffer pool, integration/image_pool.h): [first page, end page) -> the
+// registered bytes.  Their pages are reserved like a CallLocks range's: no
+// call registers over them, and no OTHER range on one of their pages counts
+// as page-locked (its owner may unregister them at any time); a range inside
+// the registered bytes does.
+struct Persist {
+  uintptr_t hi;
+  const char* p;
+  size_t n;
+};
+std::map<uintptr_t, Persist> g_persist;
+size_t g_persist_bytes = 0;
+
 // (under g_lock_mu)
-bool touches_locked(uintptr_t lo, uintptr_t hi) {
+bool touches_calls(uintptr_t lo, uintptr_t hi) {
   auto it = g_locked.lower_bound(hi);  // the first range starting at or after hi
   if (it == g_locked.begin()) return false;
   --it;
   return it->second > lo;
+}
+// the persistent registration whose pages [lo, hi) touches (nullptr: none);
+// *more: it touches more than one
+const Persist* touches_persist(uintptr_t lo, uintptr_t hi, bool* more) {
+  *more = false;
+  auto it = g_persist.lower_bound(hi);
+  const Persist* hit = nullptr;
+  while (it != g_persist.begin()) {
+    --it;
+    if (it->second.hi <= lo) break;
+    if (hit) *more = true;
+    hit = &it->second;
+  }
+  return hit;
+}
+bool touches_locked(uintptr_t lo, uintptr_t hi) {
+  bool more;
+  return touches_calls(lo, hi) || touches_persist(lo, hi, &more) != nullptr;
 }
 }  // namespace
 
 bool host_pinned(const void* p, size_t n) {
   if (!p || n == 0) return false;
   std::lock_guard<std::mutex> l(g_lock_mu);
-  if (touches_locked(page_lo(p), page_hi(p, n))) return false;
+  const uintptr_t lo = page_lo(p), hi = page_hi(p, n);
+  if (touches_calls(lo, hi)) return false;
+  bool more = false;
+  const Persist* r = touches_persist(lo, hi, &more);
+  if (r) {  // only bytes inside one registration's own bytes
+    const char* c = static_cast<const char*>(p);
+    if (more || c < r->p || c + n > r->p + r->n) return false;
+  }
   return pinned_range(p, n);
+}
+
+// lsbm_host_register: see include/lsbm_crc32c.h.
+int host_register(const void* p, size_t n) {
+  if (!p || n == 0) return -1;
+  const uintptr_t lo = page_lo(p), hi = page_hi(p, n);
+  {
+    std::lock_guard<std::mutex> l(g_lock_mu);
+    if (touches_locked(lo, hi)) return -1;  // (a live call's or another registration's pages)
+    if (g_persist_bytes + n > host_register_budget()) return -1;
+    hipPointerAttribute_t a;
+    const char* c = static_cast<const char*>(p);
+    for (const char* x : {c, c + n - 1}) {  // (never over an older registration)
+      const hipError_t e = hipPointerGetAttributes(&a, x);
+      (void)hipGetLastError();
+      if (e == hipSuccess && a.type != hipMemoryTypeUnregistered) return -1;
+    }
+    g_persist.emplace(lo, Persist{hi, c, n});  // reserved
+    g_persist_bytes += n;
+  }
+  if (hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault) == hipSuccess) return 0;
+  (void)hipGetLastError();
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  g_persist.erase(lo);
+  g_persist_bytes -= n;
+  return -1;
+}
+
+int host_unregister(const void* p) {
+  if (!p) return -1;
+  uintptr_t lo;
+  size_t n;
+  {
+    std::lock_guard<std::mutex> l(g_lock_mu);
+    auto it = g_persist.find(page_lo(p));
+    if (it == g_persist.end() || it->second.p != p) return -1;
+    lo = it->first;
+    n = it->second.n;
+  }
+  // unlocked first, then the reservation released (as ~CallLocks)
+  const hipError_t e = hipHostUnregister(const_cast<void*>(p));
+  (void)hipGetLastError();
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  g_persist.erase(lo);
+  g_persist_bytes -= n;
+  return e == hipSuccess ? 0 : -1;
+}
+
+size_t host_registered_bytes() {
+  std::lock_guard<std::mutex> l(g_lock_mu);
+  return g_persist_bytes;
 }
 
 int locked_ranges() {
@@ -617,6 +709,10 @@ void trim_idle_locked(int device, size_t keep) {
 }
 }  // namespace
 
+// Registrations through lsbm_host_register: within the same LSBM_PINNED_MB
+// (all of them together, whichever device DMAs from them).
+size_t host_register_budget() { return pinned_budget(); }
+
 size_t pinned_bytes(int device) {
   return device >= 0 && device < kMaxDevices ? g_pinned[device].load() : 0;
 }
@@ -1108,6 +1204,18 @@ extern "C" __attribute__((visibility("default"))) int lsbm_test_pool_helpers(int
       },
       max_helpers);
   return (int)ids.size();
+}
+
+extern "C" __attribute__((visibility("default"))) int lsbm_host_register(const void* p, uint64_t n) {
+  return lsbm::host_register(p, (size_t)n);
+}
+
+extern "C" __attribute__((visibility("default"))) int lsbm_host_unregister(const void* p) {
+  return lsbm::host_unregister(p);
+}
+
+extern "C" __attribute__((visibility("default"))) unsigned long long lsbm_host_registered_bytes(void) {
+  return (unsigned long long)lsbm::host_registered_bytes();
 }
 
 extern "C" __attribute__((visibility("default"))) int lsbm_test_locked_ranges(void) {

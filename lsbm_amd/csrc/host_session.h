@@ -202,6 +202,11 @@ size_t pinned_bytes(int device);
 // that stays locked for the caller's call?  Not if a page of it is held by
 // another call's CallLocks (that call unlocks it when it returns).
 bool host_pinned(const void* p, size_t n);
+// Long-lived registrations (lsbm_host_register / lsbm_host_unregister, the C
+// ABI's): 0 or -1, and the bytes registered so far.
+int host_register(const void* p, size_t n);
+int host_unregister(const void* p);
+size_t host_registered_bytes();
 
 // Page-locks a call's pageable images (hipHostRegister: ~1 us, the pages are
 // pinned by the DMA that reads them) so that they are DMA-ed in place with no

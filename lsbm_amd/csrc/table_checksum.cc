@@ -525,13 +525,8 @@ Status verify_one(int device, char* file, size_t file_size, const BlockHandle* h
 }  // namespace
 
 Status VerifyBlocks(int device, const char* file, size_t file_size, const BlockHandle* handles,
-                    size_t n, std::vector<uint8_t>* ok) {
-  return verify_one(device, const_cast<char*>(file), file_size, handles, n, ok, kImagesReadOnly);
-}
-
-Status VerifyBlocks(int device, char* file, size_t file_size, const BlockHandle* handles, size_t n,
-                    std::vector<uint8_t>* ok) {
-  return verify_one(device, file, file_size, handles, n, ok, kImagesWritable);
+                    size_t n, std::vector<uint8_t>* ok, ImageMemory memory) {
+  return verify_one(device, const_cast<char*>(file), file_size, handles, n, ok, memory);
 }
 
 }  // namespace lsbm

@@ -166,6 +166,74 @@ int oracle_batch_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len, ui
   return started == threads ? 0 : -1;
 }
 
+/* Multithreaded drivers for the full-size parity tests (every block of config 4
+ * and of a 1M-block SSTable image checked, not a sample).  Both split [0, n)
+ * into `threads` equal block ranges; each block goes through oracle_extend
+ * (util/crc32c.cc:286-329) exactly as the scalar drivers above do. */
+typedef struct {
+  const uint8_t* base;
+  const uint64_t* offsets; /* offsets: block i = [offsets[i], offsets[i+1]) - base_off */
+  const uint8_t* types;    /* sst: NULL for offsets jobs */
+  uint64_t base_off, lo, hi;
+  uint32_t* out;
+} span_job;
+
+static void* offsets_worker(void* arg) {
+  span_job* j = (span_job*)arg;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    j->out[i] = oracle_extend(0, j->base + (j->offsets[i] - j->base_off), j->offsets[i + 1] - j->offsets[i]);
+  return NULL;
+}
+
+/* table/table_builder.cc:243-249 (WriteRawBlock): the trailer's crc field is
+ * Mask(Extend(Value(block), &type, 1)).  offsets holds BlockHandle pairs
+ * {offset, size} here (table/format.h:20-47). */
+static void* sst_worker(void* arg) {
+  span_job* j = (span_job*)arg;
+  for (uint64_t i = j->lo; i < j->hi; i++) {
+    const uint64_t off = j->offsets[2 * i] - j->base_off, size = j->offsets[2 * i + 1];
+    const uint32_t crc = oracle_extend(0, j->base + off, size);
+    j->out[i] = oracle_mask(oracle_extend(crc, &j->types[i], 1));
+  }
+  return NULL;
+}
+
+static int run_spans(void* (*fn)(void*), const uint8_t* base, const uint64_t* offsets, const uint8_t* types,
+                     uint64_t base_off, uint64_t n, uint32_t* out, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  oracle_init();
+  pthread_t tid[256];
+  span_job jobs[256];
+  const uint64_t per = (n + (uint64_t)threads - 1) / (uint64_t)threads;
+  int started = 0;
+  for (int t = 0; t < threads; t++) {
+    uint64_t lo = (uint64_t)t * per, hi = lo + per;
+    if (lo > n) lo = n;
+    if (hi > n) hi = n;
+    jobs[t] = (span_job){base, offsets, types, base_off, lo, hi, out};
+    if (pthread_create(&tid[t], NULL, fn, &jobs[t]) != 0) break;
+    started++;
+  }
+  for (int t = 0; t < started; t++) pthread_join(tid[t], NULL);
+  return started == threads ? 0 : -1;
+}
+
+/* oracle_batch_offsets (init=NULL, flags=0) on `threads` pthreads, over a
+ * window of the image: base points at image byte base_off, and every block
+ * [offsets[i], offsets[i+1]) of the n must lie in the window. */
+int oracle_batch_offsets_mt(const uint8_t* base, uint64_t base_off, const uint64_t* offsets, uint64_t n,
+                            uint32_t* out, int threads) {
+  return run_spans(offsets_worker, base, offsets, NULL, base_off, n, out, threads);
+}
+
+/* The masked trailer crc of n SSTable blocks (handles {offset, size}, types
+ * per block) on `threads` pthreads, over a window as above. */
+int oracle_sst_trailers_mt(const uint8_t* base, uint64_t base_off, const uint64_t* handles, const uint8_t* types,
+                           uint64_t n, uint32_t* out, int threads) {
+  return run_spans(sst_worker, base, handles, types, base_off, n, out, threads);
+}
+
 /* ---- benchmark byte generator: 8-byte word w of a buffer is
  *      splitmix64(seed + w), stored little-endian. ---- */
 static inline uint64_t splitmix64(uint64_t x) {

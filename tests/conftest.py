@@ -40,6 +40,10 @@ class Oracle:
         lib.oracle_batch_fixed.argtypes = [vp, u64, u64, u64, vp, vp, ctypes.c_int]
         lib.oracle_batch_fixed_mt.restype = ctypes.c_int
         lib.oracle_batch_fixed_mt.argtypes = [vp, u64, u64, u64, vp, ctypes.c_int]
+        lib.oracle_batch_offsets_mt.restype = ctypes.c_int
+        lib.oracle_batch_offsets_mt.argtypes = [vp, u64, vp, u64, vp, ctypes.c_int]
+        lib.oracle_sst_trailers_mt.restype = ctypes.c_int
+        lib.oracle_sst_trailers_mt.argtypes = [vp, u64, vp, vp, u64, vp, ctypes.c_int]
         lib.oracle_fill_splitmix64.restype = None
         lib.oracle_fill_splitmix64.argtypes = [vp, u64, u64, u64]
         lib.oracle_tables.restype = None
@@ -80,6 +84,42 @@ class Oracle:
         self.lib.oracle_batch_fixed(data.ctypes.data, stride, length, n,
                                     None if ini is None else ini.ctypes.data,
                                     out.ctypes.data, 1 if masked else 0)
+        return out
+
+    @staticmethod
+    def threads():
+        """Worker threads for the multithreaded drivers: this process's CPU
+        share (a GPU box's os.cpu_count() is the whole machine's), at most 16."""
+        try:
+            n = len(os.sched_getaffinity(0))
+        except AttributeError:
+            n = os.cpu_count() or 1
+        return max(1, min(16, n))
+
+    def batch_offsets_mt(self, window, base_off, offsets):
+        """CRCs of blocks [offsets[i], offsets[i+1]) - base_off of a host window
+        (a uint8 numpy array holding image bytes [base_off, base_off + size))."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        assert n >= 0 and int(offsets[0]) >= base_off and int(offsets[-1]) - base_off <= window.size
+        out = np.empty(max(n, 0), dtype=np.uint32)
+        assert self.lib.oracle_batch_offsets_mt(window.ctypes.data, base_off, offsets.ctypes.data, n,
+                                                out.ctypes.data, self.threads()) == 0
+        return out
+
+    def sst_trailers_mt(self, window, base_off, handles, types):
+        """Mask(Extend(Value(block), type)) of every handle {offset, size}
+        (table/table_builder.cc:243-249), over a host window as above."""
+        handles = np.ascontiguousarray(handles, dtype=np.uint64)
+        types = np.ascontiguousarray(types, dtype=np.uint8)
+        n = types.size
+        assert handles.size == 2 * n
+        if n:
+            ends = handles[0::2] + handles[1::2]
+            assert int(handles[0::2].min()) >= base_off and int(ends.max()) - base_off <= window.size
+        out = np.empty(n, dtype=np.uint32)
+        assert self.lib.oracle_sst_trailers_mt(window.ctypes.data, base_off, handles.ctypes.data,
+                                               types.ctypes.data, n, out.ctypes.data, self.threads()) == 0
         return out
 
     def fill_splitmix64(self, byte_off, nbytes, seed):

@@ -142,11 +142,11 @@ int main(int argc, char** argv) {
       th.emplace_back([&, c] {
         std::vector<uint8_t> ok;
         lsbm::Status s = lsbm::VerifyBlocks(0, ts[c].img.data(), ts[c].img.size(), ts[c].h.data(),
-                                            ts[c].h.size(), &ok);
+                                            ts[c].h.size(), &ok, lsbm::kImagesWritable);
         if (!s.ok() || std::count(ok.begin(), ok.end(), 1) != (long)ok.size()) bad++;
         const size_t victim = (7 * c + 3) % ts[c].h.size();
         ts[c].img[ts[c].h[victim].offset + 11] ^= 0x20;
-        s = lsbm::VerifyBlocks(0, ts[c].img.data(), ts[c].img.size(), ts[c].h.data(), ts[c].h.size(), &ok);
+        s = lsbm::VerifyBlocks(0, ts[c].img.data(), ts[c].img.size(), ts[c].h.data(), ts[c].h.size(), &ok, lsbm::kImagesWritable);
         if (s.ok() || std::count(ok.begin(), ok.end(), 0) != 1 || ok[victim] != 0) bad++;
         ts[c].img[ts[c].h[victim].offset + 11] ^= 0x20;
       });

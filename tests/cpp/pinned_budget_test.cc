@@ -83,7 +83,7 @@ int main(int argc, char** argv) {
                                 ts[c].h.size())
                    .ok());
         std::vector<uint8_t> ok;
-        EXPECT(lsbm::VerifyBlocks(0, ts[c].img.data(), ts[c].img.size(), ts[c].h.data(), ts[c].h.size(), &ok).ok());
+        EXPECT(lsbm::VerifyBlocks(0, ts[c].img.data(), ts[c].img.size(), ts[c].h.data(), ts[c].h.size(), &ok, lsbm::kImagesWritable).ok());
         unsigned long long b = lsbm_test_pinned_bytes(0), m = seen.load();
         while (b > m && !seen.compare_exchange_weak(m, b)) {
         }

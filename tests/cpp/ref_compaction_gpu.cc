@@ -123,9 +123,7 @@ struct PooledGpuTableBuilder {
   GpuTableBuilder b;
   PooledGpuTableBuilder(const Options& opt, WritableFile* f, uint64_t target)
       : image(ImagePool::Default().Take(GpuTableBuilder::ImageBytesFor(target))),
-        b(opt, f, 0, target, &image->bytes) {
-    b.SetImageMoveObserver(&ImagePool::Moving, image);
-  }
+        b(opt, f, 0, target, &image->bytes, &ImagePool::Moving, image) {}
   ~PooledGpuTableBuilder() { ImagePool::Default().Give(image); }
   void Add(const Slice& k, const Slice& v) { b.Add(k, v); }
   Status Finish() { return b.Finish(); }

@@ -299,6 +299,87 @@ int main(int argc, char** argv) {
     delete ifp;
     delete bloom;
   }
+  // ---- a device that cannot seal or verify (lsbm_test_fail_host_pipeline:
+  // the status a copy, launch or staging error returns): the CPU fallback of
+  // integration/gpu_fallback.h, the same file bytes and the same statuses ----
+  {
+    Options opt;
+    opt.comparator = &icmp;
+    const FilterPolicy* bloom = NewBloomFilterPolicy(10);
+    InternalFilterPolicy ifp(bloom);
+    opt.filter_policy = &ifp;
+    const uint64_t target = 4u << 20;
+    Stream s(0xFA170000u);
+    std::vector<std::string> keys, vals;
+    std::string k, v;
+    for (uint64_t approx = 0; approx < target + target / 4; approx += k.size() + v.size() + 4) {
+      s.entry(&k, &v);
+      keys.push_back(k);
+      vals.push_back(v);
+    }
+    StringSink ref_file, gpu_file;
+    TableBuilder ref(opt, &ref_file);
+    GpuTableBuilder gpu(opt, &gpu_file, 0);
+    size_t used = 0;
+    for (size_t i = 0; i < keys.size() && ref.FileSize() < target; i++, used++) ref.Add(keys[i], vals[i]);
+    for (size_t i = 0; i < used; i++) gpu.Add(keys[i], vals[i]);
+    EXPECT(ref.Finish().ok());
+    const uint64_t seals0 = GpuFallbacks().seals.load();
+    EXPECT(lsbm_test_fail_host_pipeline(0) == 0);
+    const Status gs = gpu.Finish();
+    (void)lsbm_test_fail_host_pipeline(-1);
+    EXPECT(gs.ok());  // (round 5: IOError "gpu seal", a sticky bg_error_ in lsbm)
+    EXPECT(gpu.HostSeals() == 1 && GpuFallbacks().seals.load() == seals0 + 1);
+    EXPECT(gpu.LastGpuError().find("injected fault") != std::string::npos);
+    const bool same = gpu_file.data == ref_file.data;
+    EXPECT(same);
+    // the read side: the reference's verified iteration against
+    // OpenVerifiedTable with its device call failing, on the good file and on
+    // one with a flipped data-block byte
+    auto read = [&](const std::string& file, bool gpu_end, Status* st) -> size_t {
+      StringSource src(file);
+      TableImageFile* imf = nullptr;
+      Table* t = nullptr;
+      size_t nblk = 0, n = 0;
+      bool match = true;
+      ReadOptions ro;
+      if (gpu_end) {
+        EXPECT(lsbm_test_fail_host_pipeline(0) == 0);
+        *st = OpenVerifiedTable(opt, 4000, &src, file.size(), 0, &imf, &t, &nblk);
+        (void)lsbm_test_fail_host_pipeline(-1);
+      } else {
+        *st = Table::Open(opt, 4001, &src, file.size(), &t);
+        ro.verify_checksums = true;
+      }
+      if (!st->ok()) return 0;
+      Iterator* it = t->NewIterator(ro);
+      for (it->SeekToFirst(); it->Valid(); it->Next(), n++)
+        match = match && n < used && it->key() == Slice(keys[n]) && it->value() == Slice(vals[n]);
+      *st = it->status();
+      EXPECT(match);
+      delete it;
+      delete t;
+      delete imf;
+      return n;
+    };
+    const uint64_t ver0 = GpuFallbacks().verifies.load();
+    Status rst, gst;
+    const size_t rn = read(ref_file.data, false, &rst), gn = read(ref_file.data, true, &gst);
+    EXPECT(rst.ok() && gst.ok() && rn == used && gn == used);
+    EXPECT(GpuFallbacks().verifies.load() == ver0 + 1);
+    std::string bad = ref_file.data;
+    const lsbm::BlockHandle& hb = gpu.Handles()[gpu.Blocks() / 3];
+    bad[hb.offset + hb.size / 2] ^= 0x10;
+    read(bad, false, &rst);
+    read(bad, true, &gst);
+    EXPECT(GpuFallbacks().verifies.load() == ver0 + 2);
+    EXPECT(rst.IsCorruption() && rst.ToString() == gst.ToString());
+    EXPECT(gst.ToString() == "Corruption: block checksum mismatch");
+    printf("device failure: table of %zu entries, %zu blocks sealed on the CPU after \"%s\", identical=%d; "
+           "verified reads on the CPU: %s / %s\n",
+           used, gpu.Blocks(), gpu.LastGpuError().c_str(), (int)same, "OK", gst.ToString().c_str());
+    delete bloom;
+  }
   EXPECT(lsbm_test_locked_ranges() == 0);
   printf("%s tables=%zu blocks=%zu bytes=%llu ref_builder_s=%.3f gpu_builder_s=%.3f ref_verified_read_s=%.3f "
          "gpu_verified_read_s=%.3f\n",

@@ -146,7 +146,7 @@ int main(int argc, char** argv) {
     return lsbm::SealBlocks(0, base + m.off, m.size, m.h.data(), m.types.data(), m.h.size());
   };
   auto verify = [&](const Image& m, std::vector<uint8_t>* ok) {
-    return lsbm::VerifyBlocks(0, base + m.off, m.size, m.h.data(), m.h.size(), ok);  // (char*: writable)
+    return lsbm::VerifyBlocks(0, base + m.off, m.size, m.h.data(), m.h.size(), ok, lsbm::kImagesWritable);
   };
 
   Gate gate(T);
@@ -175,6 +175,64 @@ int main(int argc, char** argv) {
     EXPECT(lsbm_test_locked_ranges() == 0);
     if (fails) break;
   }
+  // Pooled images (integration/image_pool.h): half of the images
+  // kept registered through lsbm_host_register around their calls, as the
+  // pool keeps a table image, while the neighbours on their shared pages seal
+  // and verify concurrently.  A registration over a page a neighbour's call
+  // holds is refused, a neighbour on a registered image's page is staged, and
+  // every byte still comes out right.
+  long pooled = 0, refused = 0;
+  for (int r = 0; r < rounds && !fails; r++) {
+    scrub();
+    std::atomic<long> reg_ok{0}, reg_no{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t] {
+        gate.arrive();
+        std::vector<int> mine;
+        for (int i = t; i < N; i += T) mine.push_back(i);
+        std::mt19937 o(7000 * r + t);
+        std::shuffle(mine.begin(), mine.end(), o);
+        std::vector<uint8_t> ok;
+        for (int i : mine) {
+          bool reg = false;
+          if ((i + r) % 2 == 0) {
+            reg = lsbm_host_register(base + im[i].off, im[i].size) == 0;
+            (reg ? reg_ok : reg_no)++;
+          }
+          EXPECT(seal(im[i]).ok());
+          const lsbm::Status s = verify(im[i], &ok);
+          EXPECT(s.ok());
+          for (uint8_t f : ok) EXPECT(f == 1);
+          if (reg) EXPECT(lsbm_host_unregister(base + im[i].off) == 0);
+        }
+      });
+    for (auto& x : th) x.join();
+    EXPECT(memcmp(base, want.data(), total) == 0);
+    EXPECT(lsbm_test_locked_ranges() == 0 && lsbm_host_registered_bytes() == 0);
+    pooled += reg_ok.load();
+    refused += reg_no.load();
+  }
+  EXPECT(pooled > 0);
+  // the rules themselves, on two neighbours: the registered one counts as
+  // page-locked, its neighbour on the shared page does not and cannot register
+  for (int i = 1; i < N; i++) {
+    const char* a = base + im[i - 1].off;
+    const char* b = base + im[i].off;
+    if (((uintptr_t)b >> 12) != ((uintptr_t)(b - 1) >> 12) || im[i - 1].size < 64) continue;
+    EXPECT(lsbm_host_register(a, im[i - 1].size) == 0);
+    EXPECT(lsbm_test_host_pinned(a, im[i - 1].size) == 1);
+    EXPECT(lsbm_test_host_pinned(a + 7, 33) == 1);
+    EXPECT(lsbm_test_host_pinned(b, im[i].size) == 0);
+    EXPECT(lsbm_host_register(b, im[i].size) == -1);
+    EXPECT(lsbm_host_register(a, im[i - 1].size) == -1);  // (twice)
+    EXPECT(lsbm_host_unregister(a + 1) == -1);
+    EXPECT(lsbm_host_unregister(a) == 0);
+    EXPECT(lsbm_test_host_pinned(a, im[i - 1].size) == 0);
+    EXPECT(lsbm_host_register(b, im[i].size) == 0 && lsbm_host_unregister(b) == 0);
+    break;
+  }
+  EXPECT(lsbm_host_registered_bytes() == 0);
   // a flipped byte fails exactly its block, with a neighbour sealing meanwhile
   {
     const int v = N / 2;
@@ -207,8 +265,10 @@ int main(int argc, char** argv) {
   EXPECT(lsbm_test_locked_ranges() == 0);
   // (calls page-locked in place; the rest of the 2 x rounds x N + ... calls were staged
   // because a neighbour held the shared page, or a page was already registered)
-  printf("%s threads=%d images=%d bytes=%zu shared_pages=%d rounds=%d locked_calls=%ld\n", fails ? "FAILED" : "OK",
-         T, N, total, (int)shared, rounds, lsbm_test_locks_taken());
+  // (pooled: images registered around their calls; refused: registrations
+  // refused because a neighbour's call held a shared page)
+  printf("%s threads=%d images=%d bytes=%zu shared_pages=%d rounds=%d locked_calls=%ld pooled=%ld refused=%ld\n",
+         fails ? "FAILED" : "OK", T, N, total, (int)shared, rounds, lsbm_test_locks_taken(), pooled, refused);
   (void)lsbm_crc32c_shutdown();
   return fails ? 1 : 0;
 }

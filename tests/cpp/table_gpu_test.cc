@@ -220,14 +220,14 @@ int main() {
     const char* sl = getenv("LSBM_SMALL_LOCKED");
     const bool locks_on = !(al && atoi(al) == 0) && !(sl && strcmp(sl, "zc") == 0);
     const long l0 = lsbm_test_locks_taken();
-    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1);
+    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1, lsbm::kImagesWritable);
     EXPECT(st.ok() && std::count(ok1.begin(), ok1.end(), 1) == (long)h[1].size());
     const long l1 = lsbm_test_locks_taken();
     EXPECT(l1 == l0 + (locks_on ? 1 : 0));
     st = lsbm::VerifyBlocks(0, static_cast<const char*>(&f[1][0]), f[1].size(), h[1].data(), h[1].size(), &ok1);
     EXPECT(st.ok() && lsbm_test_locks_taken() == l1);
     f[1][h[1][6].offset + 2] ^= 0x02;
-    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1);
+    st = lsbm::VerifyBlocks(0, &f[1][0], f[1].size(), h[1].data(), h[1].size(), &ok1, lsbm::kImagesWritable);
     EXPECT(st.IsCorruption() && std::count(ok1.begin(), ok1.end(), 0) == 1 && ok1[6] == 0);
     f[1][h[1][6].offset + 2] ^= 0x02;
     EXPECT(lsbm_test_locked_ranges() == 0);

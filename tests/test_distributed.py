@@ -50,10 +50,20 @@ def _worker(rank, world, port, q):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item())
 
-        t_max = bench.timed_steps(step, 3, 1, lambda: None, dist.barrier, max_reduce)
+        own = {}
+
+        def max_reduce_own(x):
+            own["s"] = x
+            return max_reduce(x)
+
+        t_max = bench.timed_steps(step, 3, 1, lambda: None, dist.barrier, max_reduce_own)
         gathered = [None] * world
         dist.all_gather_object(gathered, (lo, hi, out["crc"].tolist(), t_max))
-        q.put((rank, gathered))
+        # bench.py's per-rank table over the same group
+        rec = bench.rank_record(rank, own["s"], (hi - lo) * L * 3, None,
+                                {"device": rank, "cpu_numa_nodes": bench.numa_node_of_cpus(os.sched_getaffinity(0))})
+        ranks = bench.gather_ranks(dist, world, rec)
+        q.put((rank, (gathered, ranks)))
     finally:
         dist.destroy_process_group()
 
@@ -70,8 +80,11 @@ def test_shards_partition_and_max_time():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    g = results[0]
-    assert g == results[1]
+    g, ranks = results[0]
+    assert (g, ranks) == results[1]
+    assert [r["rank"] for r in ranks] == [0, 1] and [r["device"] for r in ranks] == [0, 1]
+    assert sum(r["bytes"] for r in ranks) == 203 * 512 * 3
+    assert max(r["elapsed_s"] for r in ranks) == pytest.approx(g[0][3], abs=1e-5)  # the MAX is rank 1's
     (lo0, hi0, c0, t0), (lo1, hi1, c1, t1) = g
     assert lo0 == 0 and hi0 == lo1 and hi1 == 203  # disjoint, covering
     assert t0 == t1 and t0 >= 3 * 0.05  # MAX over ranks: the slow rank's time

@@ -39,6 +39,15 @@ def test_bench_launches_two_ranks_config5_shards(torch_cuda, oracle, tmp_path):
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["blocks_per_gpu"] == 10_000_000
     assert "over gloo" in line["config"]["parallelism"]  # the default: no RCCL in the harness
+    # the per-rank table: both ranks, their bytes add up to the aggregate, and
+    # the slowest rank's time is the reported one (MAX over ranks)
+    rk = line["ranks"]
+    assert [r["rank"] for r in rk] == [0, 1]
+    total = sum(r["bytes"] for r in rk)
+    assert total == 2 * 10_000_000 * 4096 * line["steps"]
+    t_max = max(r["elapsed_s"] for r in rk)
+    assert abs(total / t_max / 2**30 - line["value"]) <= 0.01 * line["value"]
+    assert all(r["device"] == 0 and r["GiBps"] > 0 and r["kernel_ms_per_launch"] > 0 for r in rk)
     files = sorted(glob.glob(prefix + ".rank*.npz"))
     assert len(files) == 2
     seen = []

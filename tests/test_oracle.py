@@ -78,6 +78,37 @@ def test_oracle_batch_drivers(oracle):
     assert all(fx[i] == oracle.value(data[i * 100:i * 100 + 64].tobytes()) for i in range(20))
 
 
+def test_oracle_multithreaded_window_drivers(oracle, golden):
+    """The drivers the full-size GPU parity tests use (every config-4 CRC, every
+    trailer of a 1M-block SSTable image): a window starting at image byte
+    base_off gives the scalar driver's CRCs, and the SSTable driver gives the
+    golden trailers of the reference's WriteRawBlock."""
+    rng = np.random.default_rng(2)
+    lens = rng.integers(0, 5000, size=700)
+    lens[::50] = 0
+    offs = np.zeros(701, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += 1000
+    data = stream_bytes(98, 0, int(offs[-1]) + 7)
+    full = oracle.batch_offsets(data, offs)
+    for a, b in ((0, 700), (13, 400), (699, 700), (5, 5)):
+        base = int(offs[a]) - 3
+        win = np.ascontiguousarray(data[base:int(offs[b]) + 2])
+        assert np.array_equal(oracle.batch_offsets_mt(win, base, offs[a:b + 1]), full[a:b]), (a, b)
+    # SSTable trailers over the golden blocks laid out one after another
+    blks = [printable_bytes(x["seed"], x["len"]) for x in golden["sst_blocks"]]
+    handles, img, pos = [], [], 77
+    for blk in blks:
+        handles += [pos, blk.size]
+        img.append(blk)
+        img.append(np.zeros(5, np.uint8))
+        pos += blk.size + 5
+    img = np.concatenate([np.zeros(77, np.uint8)] + img)
+    types = np.array([x["type"] for x in golden["sst_blocks"]], np.uint8)
+    got = oracle.sst_trailers_mt(img[40:], 40, np.array(handles, np.uint64), types)
+    assert [oracle.unmask(int(v)) for v in got] == [x["crc"] for x in golden["sst_blocks"]]
+
+
 def test_sse42_cpu_baseline_matches_the_oracle():
     """bench.py's "not reference" CPU line (oracle/sse42_baseline.c: the x86
     crc32 instruction, three blocks interleaved) computes crc32c::Value

@@ -256,7 +256,7 @@ int main(int argc, char** argv) {
   g_t_first = now();
   for (int r = 0; r < 3; r++) {
     s = lsbm::SealBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.types.data(), t.h.size());
-    if (s.ok()) s = lsbm::VerifyBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.h.size(), &ok);
+    if (s.ok()) s = lsbm::VerifyBlocks(0, t.img.data(), t.img.size(), t.h.data(), t.h.size(), &ok, lsbm::kImagesWritable);
   }
   if (!s.ok()) {
     fprintf(stderr, "warm-up: %s\n", s.ToString().c_str());
@@ -267,7 +267,7 @@ int main(int argc, char** argv) {
     return lsbm::SealBlocks(0, tb.img.data(), tb.img.size(), tb.h.data(), tb.types.data(), tb.h.size());
   };
   auto verify = [&](Table& tb) {
-    return lsbm::VerifyBlocks(0, tb.img.data(), tb.img.size(), tb.h.data(), tb.h.size(), &ok);
+    return lsbm::VerifyBlocks(0, tb.img.data(), tb.img.size(), tb.h.data(), tb.h.size(), &ok, lsbm::kImagesWritable);
   };
   auto phase = [&](const char* what, const std::function<lsbm::Status()>& call) {
     std::vector<double> v, starts;

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Config 1 with lsbm's own db_bench on the GPU box: the Level-2 parity test
 # (tests/test_gpu_parity.py::test_db_bench_gpu_tables), then the three builds
-# interleaved (tools/db_bench_ab.py).  Output under gpurun_out/r5_dbbench/.
+# interleaved (tools/db_bench_ab.py).  Output under gpurun_out/dbbench/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-OUT=gpurun_out/r5_dbbench; mkdir -p $OUT
+OUT=gpurun_out/dbbench; mkdir -p $OUT
 nproc > $OUT/host.txt; lscpu | grep "Model name" >> $OUT/host.txt
 timeout -k 10 300 python -u -m pytest -x -v -s --timeout 280 --timeout-method thread \
   tests/test_gpu_parity.py -k db_bench_gpu > $OUT/test.log 2>&1 || { echo "test failed"; tail -30 $OUT/test.log; exit 1; }

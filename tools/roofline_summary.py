@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Join tools/r5/roofline.sh's passes per entry (tools/roofline_all.py):
+"""Join tools/roofline.sh's passes per entry (tools/roofline_all.py):
 rocprof's average duration of the entry's kernel(s) (kernel-trace stats),
 its HBM read bytes per dispatch (FETCH_SIZE x 1024 x 2, the gfx950
 correction of MI355X_MICROARCH.md) and the entry's algorithmic bytes.
