@@ -43,7 +43,18 @@ def timeline(st, alg_bytes):
     dur = (end - start) / 100.0
     endr = (end - t0) / 100.0
     setup = (first - start) / 100.0
-    return {"waves": nw, "span_us": round(float(span), 1),
+    xcc = st[3][:nw].astype(np.int64)
+    wpw = int(os.environ.get("LSBM_WAVES_PER_WG", "16"))
+    wg = np.arange(nw) // wpw
+    ngw = nw // wpw
+    wg_end = np.array([endr[wg == g].max() for g in range(ngw)])
+    wg_in = np.array([endr[wg == g].max() - endr[wg == g].min() for g in range(ngw)])
+    by_xcc = {int(x): [round(float(endr[xcc == x].mean()), 1), round(float(dur[xcc == x].mean()), 1)]
+              for x in np.unique(xcc)}
+    extra = {"by_xcc_mean_end_dur_us": by_xcc,
+             "wg_end_p0_p50_p100_us": [round(float(x), 1) for x in np.percentile(wg_end, [0, 50, 100])],
+             "within_wg_end_spread_mean_us": round(float(wg_in.mean()), 1)}
+    return {"waves": nw, **extra, "span_us": round(float(span), 1),
             "GBps_span": round(alg_bytes / (span / 1e6) / 1e9, 1),
             "pct_hbm_span": round(100 * alg_bytes / (span / 1e6) / 8e12, 2),
             "start_spread_us": round(float((start - t0).max() / 100.0), 1),
@@ -66,10 +77,15 @@ def run(entry, lb, stamps_fn, launch, alg, reps=3):
     for r in range(reps):
         launch()
         torch.cuda.synchronize()
+        st[:] = 0
         assert stamps_fn(st.ctypes.data, 4 * 65536) == 0
         rec = {"entry": entry, "rep": r, "algorithmic_bytes": int(alg)}
         rec.update(timeline(st, alg))
         print(json.dumps(rec), flush=True)
+        dump = os.environ.get("LSBM_STAMPS_DUMP")  # a directory: the raw stamps per entry and rep
+        if dump:
+            os.makedirs(dump, exist_ok=True)
+            np.save(os.path.join(dump, f"{entry}_{r}.npy"), st[:, :rec["waves"]])
 
 
 def main():
