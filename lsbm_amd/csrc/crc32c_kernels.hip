@@ -118,7 +118,12 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     uint32_t k = 0;
     if (lane == 0) k = atomicAdd(&s_next, 1u);
     k = __builtin_amdgcn_readfirstlane(k);
+#ifdef LSBM_WG_ROTATE  // A/B: row c of the interleave rotated by c workgroups
+    const uint64_t c = k / kWavesPerWg;
+    return c * nwaves + (((uint64_t)blockIdx.x + c) % gridDim.x) * kWavesPerWg + (k % kWavesPerWg);
+#else
     return (uint64_t)(k / kWavesPerWg) * nwaves + (uint64_t)blockIdx.x * kWavesPerWg + (k % kWavesPerWg);
+#endif
   };
 #else
   auto next_grp = [&](uint64_t gp) -> uint64_t { return gp + nwaves; };

@@ -6,7 +6,7 @@
 set -e
 NAME=$1; SRC=$2; DEFS=$3
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-D=$ROOT/build/abl/$NAME; mkdir -p $D
+D=${ABL_DIR:-$ROOT/build/abl}/$NAME; mkdir -p $D
 make -s -C $ROOT/lsbm_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -fvisibility=hidden \
   -munsafe-fp-atomics -DLSBM_DIAG_BUILD $DEFS -c -o $D/$SRC.o $ROOT/lsbm_amd/csrc/$SRC.hip

@@ -95,9 +95,13 @@ def main():
     torch.cuda.set_device(0)
     engine.init(0)
     lb = lib()
+    fns = []
     for name in ("lsbm_diag_stamps", "lsbm_diag_stamps_stream"):
-        getattr(lb, name).argtypes = [ctypes.c_void_p, ctypes.c_int]
-    units, stream = lb.lsbm_diag_stamps, lb.lsbm_diag_stamps_stream
+        f = getattr(lb, name, None)  # (a variant may stamp one kernel source only)
+        if f is not None:
+            f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        fns.append(f)
+    units, stream = fns
     entries = sys.argv[1:] or ["config4", "sst_verify", "sst_crcs", "sst_seal", "fixed4k"]
     s = torch.cuda.current_stream()
     if "fixed4k" in entries:
