@@ -30,7 +30,8 @@ namespace lsbm {
 // launchers (crc32c_kernels.hip)
 hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uint64_t n_blocks,
                         const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
-                        const DevConsts* dc, int grid, hipStream_t stream);
+                        const DevConsts* dc, int grid, hipStream_t stream,
+                        uint32_t* heads);
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream);
 bool ragged_uses_stream(const RaggedArgs& a);
 int set_ragged_policy(int p);
@@ -229,6 +230,22 @@ uint64_t fixed_split_blocks() {
   return b;
 }
 
+// The fixed kernel's cross-XCC work queue (crc32c_units.h): LSBM_FIXED_QUEUE=0
+// keeps the static interleave (A/B).  Only for launches of at least 4 groups
+// per wave, and never while the stream is being captured into a graph (the
+// heads are per-call scratch).
+std::atomic<int> g_fixed_queue{-1};  // -1: not read yet; 0 off, 1 on (lsbm_test_fixed_queue)
+bool fixed_queue_on() {
+  int q = g_fixed_queue.load(std::memory_order_relaxed);
+  if (q < 0) {
+    const char* v = getenv("LSBM_FIXED_QUEUE");
+    q = (v && v[0] == '0') ? 0 : 1;
+    int expect = -1;
+    if (!g_fixed_queue.compare_exchange_strong(expect, q)) q = expect;
+  }
+  return q == 1;
+}
+
 int grid_for(const DeviceState* st, uint64_t n_blocks) {
   const uint64_t groups = (n_blocks + 7) / 8;
   const uint64_t wgs = (groups + kWavesPerWg - 1) / kWavesPerWg;
@@ -318,6 +335,14 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
 
 }  // namespace
 
+// Testing (include/lsbm_crc32c.h): the fixed kernel's cross-XCC queue on (1)
+// or off (0: the static interleave); -1 back to LSBM_FIXED_QUEUE's default.
+extern "C" __attribute__((visibility("default"))) int lsbm_test_fixed_queue(int on) {
+  if (on < -1 || on > 1) return -1;
+  g_fixed_queue.store(on);
+  return 0;
+}
+
 // engine_internal.h: shared with the bloom entry points (bloom_engine.cc)
 int engine_fail(int code, const char* what) { return fail(code, what); }
 int engine_fail_hip(hipError_t e, const char* what) { return fail_hip(e, what); }
@@ -393,14 +418,40 @@ __attribute__((visibility("default"))) int lsbm_crc32c_fixed_dev(
     // on the caller's stream (one launch over a 10M-block
     // shard ran 1-2 points under the same blocks a million at a time).
     const uint64_t per = fixed_split_blocks();
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    // the launches, and whether they take their groups from a cross-XCC queue:
+    // one set of heads per launch, zeroed here, in stream-ordered scratch
+    uint64_t launches = 0, min_m = n_blocks;
+    for (uint64_t f = 0; f < n_blocks; launches++) {
+      const uint64_t m = (per && n_blocks - f >= 2 * per) ? per : n_blocks - f;
+      min_m = std::min(min_m, m);
+      f += m;
+    }
+    uint32_t* heads = nullptr;
+    const uint64_t nwaves = (uint64_t)st->num_cus * kWavesPerWg;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (fixed_queue_on() && (min_m + 7) / 8 >= 4 * nwaves && hipStreamIsCapturing(hs, &cap) == hipSuccess &&
+        cap == hipStreamCaptureStatusNone) {
+      const size_t bytes = launches * kQueueWords * sizeof(uint32_t);
+      if (hipMallocAsync(reinterpret_cast<void**>(&heads), bytes, hs) != hipSuccess) {
+        (void)hipGetLastError();
+        heads = nullptr;
+      } else if (hipMemsetAsync(heads, 0, bytes, hs) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFreeAsync(heads, hs);
+        heads = nullptr;
+      }
+    }
     hipError_t e = hipSuccess;
-    for (uint64_t f = 0; f < n_blocks && e == hipSuccess;) {
+    uint64_t li = 0;
+    for (uint64_t f = 0; f < n_blocks && e == hipSuccess; li++) {
       const uint64_t m = (per && n_blocks - f >= 2 * per) ? per : n_blocks - f;
       e = launch_fixed(static_cast<const uint8_t*>(d_base) + f * stride, stride,
                        (uint32_t)(len / kRowBytes), m, d_init ? d_init + f : nullptr, d_out + f, flags,
-                       k_value, st->d_consts, grid_for(st, m), static_cast<hipStream_t>(stream));
+                       k_value, st->d_consts, grid_for(st, m), hs, heads ? heads + li * kQueueWords : nullptr);
       f += m;
     }
+    if (heads) (void)hipFreeAsync(heads, hs);
     return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_fixed_kernel");
   }
   // Any other geometry: the ragged kernel with fixed-stride extents.

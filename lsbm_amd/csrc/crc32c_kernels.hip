@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t rows_arg, uint64_t n_blocks,
     const uint32_t* __restrict__ init, uint32_t* __restrict__ out, uint32_t flags,
     uint32_t k_value /* A^len(~0) ^ ~0: the init term of crc32c::Value */,
-    const DevConsts* __restrict__ dc) {
+    const DevConsts* __restrict__ dc, uint32_t* __restrict__ heads /* null: no cross-XCC queue */) {
   const uint32_t rows = kRows ? kRows : rows_arg;  // kRows != 0: fully unrolled
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 3, li = lane & 7u;
@@ -138,8 +138,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
   load_lds_tables(g_lds, dc);
   DIAG_STAMP(1);
 
+  // With the cross-XCC queue (crc32c_units.h): every wave's first group is
+  // its own (row 0 of the interleave), the rest come from the heads.
+  uint32_t qh = heads ? xcc_id() : 0u, q_pend = 0, q_out = 0;
   bool first = true;
-  for (; grp < ngroups; grp = next_grp(grp)) {
+  while (grp < ngroups) {
     const uint64_t blk = grp * 8 + g;
     const bool valid = blk < n_blocks;
     // Two banks of kPF rows: while one bank is absorbed the other's loads
@@ -151,6 +154,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
       if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
     }
     first = false;
+    if (heads) q_pend = queue_issue(heads, qh);  // the next group, behind this one's first loads
     uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
 #pragma unroll
     for (uint32_t k = 1; k < kPF; k++)
@@ -179,6 +183,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
         crc = raw ^ k_value;
       out[blk] = (flags & 1u) ? mask_crc(crc) : crc;
     }
+    grp = heads ? queue_resolve(heads, qh, q_pend, nwaves, ngroups, q_out) : next_grp(grp);
   }
   DIAG_STAMP(2);
   DIAG_XCC_W(wave);
@@ -369,10 +374,10 @@ __global__ __launch_bounds__(kBlockThreads) void stream_read_kernel(const uint8_
 // ---- host-callable launchers (C++ linkage, used by crc32c_engine.cc) ----
 hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t rows, uint64_t n_blocks,
                         const uint32_t* init, uint32_t* out, uint32_t flags, uint32_t k_value,
-                        const DevConsts* dc, int grid, hipStream_t stream) {
+                        const DevConsts* dc, int grid, hipStream_t stream, uint32_t* heads) {
 #define LSBM_LAUNCH_FIXED(HI, R)                                                        \
   hipLaunchKernelGGL((crc32c_fixed_kernel<HI, R>), dim3(grid), dim3(kBlockThreads), 0, stream, \
-                     base, stride, rows, n_blocks, init, out, flags, k_value, dc)
+                     base, stride, rows, n_blocks, init, out, flags, k_value, dc, heads)
   // compile-time row counts for the SSTable-sized configs: 4 KiB and 64 KiB
   if (init) {
     if (rows == 32) LSBM_LAUNCH_FIXED(true, 32);

@@ -72,6 +72,12 @@ constexpr uint32_t kLdsWords = kLdsBytes / 4;
 // take pieces from one.  Reserved here, so that a table added to the image
 // fails this assert rather than hipcc's LDS limit on some kernel.
 constexpr uint32_t kLdsKernelWords = 4;
+
+// The cross-XCC work queue's heads (crc32c_units.h): one word per XCC, each
+// on its own 64-B line; kQueueWords words of scratch per launch.
+constexpr uint32_t kQueueHeads = 8;
+constexpr uint32_t kQueueStride = 16;
+constexpr uint32_t kQueueWords = kQueueHeads * kQueueStride;
 static_assert(kLdsBytes % 16 == 0 && kLdsBytes + 4u * kLdsKernelWords <= 160u * 1024u,
               "one LDS image per CU, plus the kernels' work counters");
 static_assert(kStreamHM % 16 == 0, "ds_read_b128 of a mask");

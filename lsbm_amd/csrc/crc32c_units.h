@@ -14,6 +14,53 @@ namespace lsbm {
 
 __shared__ uint32_t g_lds[kLdsWords];
 
+// ---------------------------------------------------------------------------
+// Cross-XCC work queue (round 6).  The eight XCDs of an MI355X do not read HBM
+// at one rate: with every CU streaming, the waves of some XCDs (measured: the
+// odd-numbered ones, 7% on average, 0-12% launch to launch) finish their
+// share of a statically split batch tens of microseconds after the others,
+// while within one XCD all workgroups end within ~10 us
+// (tools/wave_spread_ragged.py).  No static split can
+// know which XCD is slow, so the items past the first row are handed out at
+// run time: one head word per XCC (kQueueHeads, each on its own 64-B line),
+// head x hands out items base + 8 j + x, j = 0, 1, ... (at any moment every
+// XCD streams the same window of the batch), and a wave whose head is
+// exhausted moves on to the next head, so the fast XCDs take the slow ones'
+// last items.  One returning device-scope atomicAdd per item, issued one
+// item ahead so that its latency (~1 us with every CU streaming) is hidden
+// behind the item's rows.  The heads are zeroed before each launch (stream-
+// ordered scratch, crc32c_engine.cc).
+// ---------------------------------------------------------------------------
+// (kQueueHeads, kQueueStride, kQueueWords: crc32c_types.h)
+
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x & (kQueueHeads - 1);
+}
+
+// One claim from head h, issued by lane 0: the raw counter value (lane 0's
+// register; read it with readfirstlane when it is needed).
+__device__ __forceinline__ uint32_t queue_issue(uint32_t* heads, uint32_t h) {
+  uint32_t j = 0;
+  if ((threadIdx.x & 63u) == 0) j = atomicAdd(heads + h * kQueueStride, 1u);
+  return j;
+}
+
+// Resolve a claim issued on head h: the item, or, when head h is exhausted,
+// claims from the next heads in turn (h moves with them: a head once found
+// exhausted stays so); `total` when every head is.  Items are base + 8 j + h.
+__device__ __forceinline__ uint64_t queue_resolve(uint32_t* heads, uint32_t& h, uint32_t pending, uint64_t base,
+                                                  uint64_t total, uint32_t& exhausted) {
+  uint64_t item = base + (uint64_t)__builtin_amdgcn_readfirstlane(pending) * kQueueHeads + h;
+  while (item >= total) {
+    if (++exhausted >= kQueueHeads) return total;
+    h = (h + 1) & (kQueueHeads - 1);
+    item = base + (uint64_t)__builtin_amdgcn_readfirstlane(queue_issue(heads, h)) * kQueueHeads + h;
+  }
+  return item;
+}
+
 // Diagnostic builds only (-DLSBM_DIAG_STAMPS, tools/wave_spread.py): every
 // wave stamps its start (0), its first data (1) and its end (2) with
 // s_memrealtime (100 MHz), and its XCC (3).  One array per kernel source

@@ -66,6 +66,32 @@ def test_fixed_batch_split_into_launches(torch_cuda, oracle, use_init, masked):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("n", [131_072 + 3, 300_001, 1_048_576])
+@pytest.mark.parametrize("use_init,masked", [(False, False), (True, True)])
+def test_fixed_cross_xcc_queue(torch_cuda, oracle, product_lib, n, use_init, masked):
+    """The fixed kernel's cross-XCC work queue (crc32c_units.h): past the first
+    row every group is claimed at run time from the per-XCC heads, the fast
+    XCDs taking the slow ones' last groups.  Every block (the stealing tail
+    and a partial last group included) matches the oracle, with the queue on
+    and with the static interleave, and the two agree."""
+    torch = torch_cuda
+    from lsbm_amd import engine
+    length, stride = 256, 272
+    data = stream_bytes(0x51DE + n, 0, (n - 1) * stride + length)
+    rng = np.random.default_rng(n)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if use_init else None
+    d = _dev(torch, data)
+    di = _dev(torch, init, torch.int32) if use_init else None
+    want = oracle.batch_fixed(data, stride, length, n, init, masked)
+    try:
+        for on in (1, 0, 1):
+            assert product_lib.lsbm_test_fixed_queue(on) == 0
+            got = _u32(engine.crc32c_fixed(d, stride, length, n, init=di, masked=masked))
+            assert np.array_equal(got, want), on
+    finally:
+        product_lib.lsbm_test_fixed_queue(-1)
+
+
 @pytest.mark.parametrize("length,stride,n,shift", [
     (4118, 4118, 64, 0), (4117, 4123, 31, 0), (1, 1, 100, 0), (0, 16, 5, 0), (100, 100, 77, 0),
     (4096, 4096, 20, 3), (4096, 4100, 20, 0), (70000, 70001, 5, 1), (3, 5, 1000, 0),
