@@ -140,7 +140,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 
   // With the cross-XCC queue (crc32c_units.h): every wave's first group is
   // its own (row 0 of the interleave), the rest come from the heads.
+  // An item is kQueueItem consecutive groups; the next item is claimed when
+  // the first group of the current one starts.
+  const uint64_t q_items = ngroups > nwaves ? (ngroups - nwaves + kQueueItem - 1) / kQueueItem : 0;
   uint32_t qh = heads ? xcc_id() : 0u, q_pend = 0, q_out = 0;
+  uint64_t q_end = grp + 1;  // the end of the current item (the first row: one group)
   bool first = true;
   while (grp < ngroups) {
     const uint64_t blk = grp * 8 + g;
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
       if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
     }
     first = false;
-    if (heads) q_pend = queue_issue(heads, qh);  // the next group, behind this one's first loads
+    if (heads && grp + 1 >= q_end) q_pend = queue_issue(heads, qh);  // the next item, behind these loads
     uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
 #pragma unroll
     for (uint32_t k = 1; k < kPF; k++)
@@ -183,7 +187,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
         crc = raw ^ k_value;
       out[blk] = (flags & 1u) ? mask_crc(crc) : crc;
     }
-    grp = heads ? queue_resolve(heads, qh, q_pend, nwaves, ngroups, q_out) : next_grp(grp);
+    if (!heads) {
+      grp = next_grp(grp);
+    } else if (++grp >= q_end || grp >= ngroups) {
+      const uint64_t it = queue_resolve(heads, qh, q_pend, 0, q_items, q_out);
+      grp = it < q_items ? nwaves + it * kQueueItem : ngroups;
+      q_end = grp + kQueueItem;
+    }
   }
   DIAG_STAMP(2);
   DIAG_XCC_W(wave);

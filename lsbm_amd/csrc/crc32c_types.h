@@ -75,9 +75,16 @@ constexpr uint32_t kLdsKernelWords = 4;
 
 // The cross-XCC work queue's heads (crc32c_units.h): one word per XCC, each
 // on its own 64-B line; kQueueWords words of scratch per launch.
+#ifndef LSBM_QUEUE_STRIDE  // (A/B builds override)
+#define LSBM_QUEUE_STRIDE 16
+#endif
+#ifndef LSBM_QUEUE_ITEM
+#define LSBM_QUEUE_ITEM 1
+#endif
 constexpr uint32_t kQueueHeads = 8;
-constexpr uint32_t kQueueStride = 16;
+constexpr uint32_t kQueueStride = LSBM_QUEUE_STRIDE;
 constexpr uint32_t kQueueWords = kQueueHeads * kQueueStride;
+constexpr uint32_t kQueueItem = LSBM_QUEUE_ITEM;  // fixed kernel: groups per queue item
 static_assert(kLdsBytes % 16 == 0 && kLdsBytes + 4u * kLdsKernelWords <= 160u * 1024u,
               "one LDS image per CU, plus the kernels' work counters");
 static_assert(kStreamHM % 16 == 0, "ds_read_b128 of a mask");
