@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
   // the first group of the current one starts.
   const uint64_t q_items = ngroups > nwaves ? (ngroups - nwaves + kQueueItem - 1) / kQueueItem : 0;
   uint32_t qh = heads ? xcc_id() : 0u, q_pend = 0, q_out = 0;
-  uint64_t q_end = grp + 1;  // the end of the current item (the first row: one group)
+  uint64_t q_start = grp, q_end = grp + 1;  // the current item (the first row: one group)
   bool first = true;
   while (grp < ngroups) {
     const uint64_t blk = grp * 8 + g;
@@ -158,7 +158,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
       if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
     }
     first = false;
-    if (heads && grp + 1 >= q_end) q_pend = queue_issue(heads, qh);  // the next item, behind these loads
+    // (at the item's first group, so that every resolve below consumes the
+    // claim issued for it, whether or not the item ends early at ngroups)
+    if (heads && grp == q_start) q_pend = queue_issue(heads, qh);  // the next item, behind these loads
     uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
 #pragma unroll
     for (uint32_t k = 1; k < kPF; k++)
@@ -192,6 +194,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     } else if (++grp >= q_end || grp >= ngroups) {
       const uint64_t it = queue_resolve(heads, qh, q_pend, 0, q_items, q_out);
       grp = it < q_items ? nwaves + it * kQueueItem : ngroups;
+      q_start = grp;
       q_end = grp + kQueueItem;
     }
   }
