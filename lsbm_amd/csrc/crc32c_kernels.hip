@@ -140,11 +140,10 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 
   // With the cross-XCC queue (crc32c_units.h): every wave's first group is
   // its own (row 0 of the interleave), the rest come from the heads.
-  // An item is kQueueItem consecutive groups; the next item is claimed when
-  // the first group of the current one starts.
+  // An item is kQueueItem consecutive groups.
   const uint64_t q_items = ngroups > nwaves ? (ngroups - nwaves + kQueueItem - 1) / kQueueItem : 0;
   uint32_t qh = heads ? xcc_id() : 0u, q_pend = 0, q_out = 0;
-  uint64_t q_start = grp, q_end = grp + 1;  // the current item (the first row: one group)
+  uint64_t q_end = grp + 1;  // the end of the current item (the first row: one group)
   bool first = true;
   while (grp < ngroups) {
     const uint64_t blk = grp * 8 + g;
@@ -158,23 +157,44 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
       if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
     }
     first = false;
-    // (at the item's first group, so that every resolve below consumes the
-    // claim issued for it, whether or not the item ends early at ngroups)
-    if (heads && grp == q_start) q_pend = queue_issue(heads, qh);  // the next item, behind these loads
+    // The next item is claimed in the last group of this one (whether it ends
+    // at q_end or early at ngroups: every resolve below consumes the claim
+    // issued for its own item), right after the group's LAST row loads: a
+    // returning atomic retires in order with the loads (vmcnt), so one issued
+    // in front of row loads holds up the wait for each of them by its own
+    // latency (~3 us under load; measured: claims behind a group's first
+    // loads cost 9-16% of the rate).  Behind the last loads only the group's
+    // remaining rows and its finish overlap it.
+    const bool q_last = heads && (grp + 1 == q_end || grp + 1 == ngroups);
+    bool q_issued = false;  // (exactly one claim per item: a second would lose the first's item)
+    auto q_claim = [&]() {
+      if (q_last && !q_issued) {
+        q_pend = queue_issue(heads, qh);
+        q_issued = true;
+      }
+    };
+    if (rows <= 2 * kPF) q_claim();  // (both banks above were the group's only loads)
     uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
 #pragma unroll
     for (uint32_t k = 1; k < kPF; k++)
       if (k < rows) STEP_ROW(a[k]);
     uint32_t r = kPF;
     while (r < rows) {
-      if (kRows == 0 || r + kPF < rows) LOAD_BANK(a, r + kPF);
+      if (kRows == 0 || r + kPF < rows) {
+        LOAD_BANK(a, r + kPF);
+        if (r + 2 * kPF >= rows) q_claim();
+      }
       ABSORB(b, r);
       r += kPF;
       if (r >= rows) break;
-      if (kRows == 0 || r + kPF < rows) LOAD_BANK(b, r + kPF);
+      if (kRows == 0 || r + kPF < rows) {
+        LOAD_BANK(b, r + kPF);
+        if (r + 2 * kPF >= rows) q_claim();
+      }
       ABSORB(a, r);
       r += kPF;
     }
+    q_claim();  // (no-op when a load above claimed)
 #ifdef LSBM_ABL_NO_MERGE  // diagnostic builds only (tools/ablate.sh)
     const uint32_t raw = c0 ^ c1 ^ c2 ^ c3;
 #else
@@ -194,7 +214,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
     } else if (++grp >= q_end || grp >= ngroups) {
       const uint64_t it = queue_resolve(heads, qh, q_pend, 0, q_items, q_out);
       grp = it < q_items ? nwaves + it * kQueueItem : ngroups;
-      q_start = grp;
       q_end = grp + kQueueItem;
     }
   }

@@ -2,8 +2,9 @@
 crc32c_units.h queue_issue / queue_resolve), restated step for step on the
 CPU: waves run in random order; each wave's first group is its own (row 0 of
 the interleave); past it, items of k groups are claimed from 8 per-XCC heads
-(head h hands out items 8 j + h), one claim issued at the first group of the
-current item and resolved after its last, and a wave whose head is exhausted
+(head h hands out items 8 j + h), one claim issued in the last group of the
+current item (behind its last row loads; the item may end early at the batch
+end) and resolved after it, and a wave whose head is exhausted
 moves on to the next head.  Every group must be processed exactly once,
 every resolve must consume the claim issued for its own item (no stale
 claim: round 6's first multi-group version re-resolved one and looped), and
@@ -17,7 +18,7 @@ def simulate(ngroups, nwaves, k, seed):
     rnd = random.Random(seed)
     heads = [0] * 8
     q_items = (ngroups - nwaves + k - 1) // k if ngroups > nwaves else 0
-    waves = [dict(grp=w, qh=rnd.randrange(8), pend=None, out=0, q_start=w, q_end=w + 1, steps=0)
+    waves = [dict(grp=w, qh=rnd.randrange(8), pend=None, out=0, q_end=w + 1, steps=0)
              for w in range(nwaves)]
     seen = [0] * ngroups
 
@@ -44,15 +45,15 @@ def simulate(ngroups, nwaves, k, seed):
         wv["steps"] += 1
         assert wv["steps"] < 10 * ngroups + 100, "no progress"
         g = wv["grp"]
-        if g == wv["q_start"]:
-            assert wv["pend"] is None
+        if g + 1 == wv["q_end"] or g + 1 == ngroups:  # q_last: the item's last group
+            assert wv["pend"] is None, "two claims for one item"
             wv["pend"] = issue(wv["qh"])
         seen[g] += 1
         wv["grp"] += 1
         if wv["grp"] >= wv["q_end"] or wv["grp"] >= ngroups:
             it = resolve(wv)
             wv["grp"] = nwaves + it * k if it < q_items else ngroups
-            wv["q_start"], wv["q_end"] = wv["grp"], wv["grp"] + k
+            wv["q_end"] = wv["grp"] + k
         if wv["grp"] >= ngroups:
             active.remove(wv)
     return seen
