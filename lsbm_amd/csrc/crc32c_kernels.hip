@@ -128,94 +128,89 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 #else
   auto next_grp = [&](uint64_t gp) -> uint64_t { return gp + nwaves; };
 #endif
+  // With the cross-XCC queue (crc32c_units.h): row 0 is the waves' own, the
+  // rest comes in workgroup batches of W groups (items) from the heads.
+  __shared__ uint32_t s_wq[kWqWords];
+  const WgQueue<kWavesPerWg> wq{heads, (lds_u32*)s_wq,
+                                ngroups > nwaves ? (ngroups - nwaves + kWavesPerWg - 1) / kWavesPerWg : 0};
+  if (heads && threadIdx.x == 0) wq.init(xcc_id());  // (ordered by load_lds_tables' barrier)
+
   uint64_t grp = wave;
   DIAG_STAMP(0);
+  bool loaded = false;  // the banks hold grp's first rows already
   if (grp < ngroups) {
     set_group(grp);
     LOAD_BANK(a, 0);
     if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
+    loaded = true;
   }
   load_lds_tables(g_lds, dc);
   DIAG_STAMP(1);
 
-  // With the cross-XCC queue (crc32c_units.h): every wave's first group is
-  // its own (row 0 of the interleave), the rest come from the heads.
-  // An item is kQueueItem consecutive groups.
-  const uint64_t q_items = ngroups > nwaves ? (ngroups - nwaves + kQueueItem - 1) / kQueueItem : 0;
-  uint32_t qh = heads ? xcc_id() : 0u, q_pend = 0, q_out = 0;
-  uint64_t q_end = grp + 1;  // the end of the current item (the first row: one group)
-  bool first = true;
-  while (grp < ngroups) {
-    const uint64_t blk = grp * 8 + g;
-    const bool valid = blk < n_blocks;
-    // Two banks of kPF rows: while one bank is absorbed the other's loads
-    // are in flight.  Row 0 initialises the braids (c = w); every later row
-    // is c = A^128(c) ^ w.
-    if (!first) {
-      set_group(grp);
-      LOAD_BANK(a, 0);
-      if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
-    }
-    first = false;
-    // The next item is claimed in the last group of this one (whether it ends
-    // at q_end or early at ngroups: every resolve below consumes the claim
-    // issued for its own item), right after the group's LAST row loads: a
-    // returning atomic retires in order with the loads (vmcnt), so one issued
-    // in front of row loads holds up the wait for each of them by its own
-    // latency (~3 us under load; measured: claims behind a group's first
-    // loads cost 9-16% of the rate).  Behind the last loads only the group's
-    // remaining rows and its finish overlap it.
-    const bool q_last = heads && (grp + 1 == q_end || grp + 1 == ngroups);
-    bool q_issued = false;  // (exactly one claim per item: a second would lose the first's item)
-    auto q_claim = [&]() {
-      if (q_last && !q_issued) {
-        q_pend = queue_issue(heads, qh);
-        q_issued = true;
+  uint32_t pend_pub = heads && wave_in_wg == 0 ? kWqLead : 0u;  // a batch this wave publishes
+  for (;;) {
+    if (grp < ngroups) {
+      const uint64_t blk = grp * 8 + g;
+      const bool valid = blk < n_blocks;
+      // Two banks of kPF rows: while one bank is absorbed the other's loads
+      // are in flight.  Row 0 initialises the braids (c = w); every later row
+      // is c = A^128(c) ^ w.
+      if (!loaded) {
+        set_group(grp);
+        LOAD_BANK(a, 0);
+        if (kRows == 0 || kPF < rows) LOAD_BANK(b, kPF);
       }
-    };
-    if (rows <= 2 * kPF) q_claim();  // (both banks above were the group's only loads)
-    uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
+      loaded = false;
+      if (pend_pub) {  // (behind this group's first loads: the claim's wait overlaps them)
+        wq.publish(pend_pub);
+        pend_pub = 0;
+      }
+      uint32_t c0 = a[0].x, c1 = a[0].y, c2 = a[0].z, c3 = a[0].w;
 #pragma unroll
-    for (uint32_t k = 1; k < kPF; k++)
-      if (k < rows) STEP_ROW(a[k]);
-    uint32_t r = kPF;
-    while (r < rows) {
-      if (kRows == 0 || r + kPF < rows) {
-        LOAD_BANK(a, r + kPF);
-        if (r + 2 * kPF >= rows) q_claim();
+      for (uint32_t k = 1; k < kPF; k++)
+        if (k < rows) STEP_ROW(a[k]);
+      uint32_t r = kPF;
+      while (r < rows) {
+        if (kRows == 0 || r + kPF < rows) LOAD_BANK(a, r + kPF);
+        ABSORB(b, r);
+        r += kPF;
+        if (r >= rows) break;
+        if (kRows == 0 || r + kPF < rows) LOAD_BANK(b, r + kPF);
+        ABSORB(a, r);
+        r += kPF;
       }
-      ABSORB(b, r);
-      r += kPF;
-      if (r >= rows) break;
-      if (kRows == 0 || r + kPF < rows) {
-        LOAD_BANK(b, r + kPF);
-        if (r + 2 * kPF >= rows) q_claim();
-      }
-      ABSORB(a, r);
-      r += kPF;
-    }
-    q_claim();  // (no-op when a load above claimed)
 #ifdef LSBM_ABL_NO_MERGE  // diagnostic builds only (tools/ablate.sh)
-    const uint32_t raw = c0 ^ c1 ^ c2 ^ c3;
+      const uint32_t raw = c0 ^ c1 ^ c2 ^ c3;
 #else
-    const uint32_t raw = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
+      const uint32_t raw = merge_braids(g_lds, c0, c1, c2, c3, lane_fin);
 #endif
-    if (li == 7u && valid) {
-      uint32_t crc;
-      if (kHasInit)
-        crc = raw ^ advance_glb(dc, init[blk] ^ 0xffffffffu, (uint64_t)rows * kRowBytes) ^
-              0xffffffffu;
-      else
-        crc = raw ^ k_value;
-      out[blk] = (flags & 1u) ? mask_crc(crc) : crc;
+      if (li == 7u && valid) {
+        uint32_t crc;
+        if (kHasInit)
+          crc = raw ^ advance_glb(dc, init[blk] ^ 0xffffffffu, (uint64_t)rows * kRowBytes) ^
+                0xffffffffu;
+        else
+          crc = raw ^ k_value;
+        out[blk] = (flags & 1u) ? mask_crc(crc) : crc;
+      }
+    } else if (pend_pub) {
+      wq.publish(pend_pub);
+      pend_pub = 0;
     }
     if (!heads) {
       grp = next_grp(grp);
-    } else if (++grp >= q_end || grp >= ngroups) {
-      const uint64_t it = queue_resolve(heads, qh, q_pend, 0, q_items, q_out);
-      grp = it < q_items ? nwaves + it * kQueueItem : ngroups;
-      q_end = grp + kQueueItem;
+      if (grp >= ngroups) break;
+      continue;
     }
+    // the next slot: wave-group `slot` of batch `bt`
+    const uint32_t k = wq.take(), bt = k / kWavesPerWg, slot = k % kWavesPerWg;
+    if (slot == 0) pend_pub = bt + kWqLead;
+    const uint32_t it = wq.read(bt);
+    if (it == kWqNone) {
+      if (pend_pub) wq.publish(pend_pub);  // (kWqNone as well; no wave of this workgroup waits for it)
+      break;
+    }
+    grp = nwaves + (uint64_t)it * kWavesPerWg + slot;  // (past ngroups in the last item: a slot without a group)
   }
   DIAG_STAMP(2);
   DIAG_XCC_W(wave);

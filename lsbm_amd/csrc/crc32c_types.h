@@ -71,20 +71,16 @@ constexpr uint32_t kLdsWords = kLdsBytes / 4;
 // counter (s_next, crc32c_kernels.hip) -- and the ragged kernels' once they
 // take pieces from one.  Reserved here, so that a table added to the image
 // fails this assert rather than hipcc's LDS limit on some kernel.
-constexpr uint32_t kLdsKernelWords = 4;
+constexpr uint32_t kLdsKernelWords = 20;  // (fixed kernel: s_next and the WgQueue words)
 
 // The cross-XCC work queue's heads (crc32c_units.h): one word per XCC, each
 // on its own 64-B line; kQueueWords words of scratch per launch.
 #ifndef LSBM_QUEUE_STRIDE  // (A/B builds override)
 #define LSBM_QUEUE_STRIDE 16
 #endif
-#ifndef LSBM_QUEUE_ITEM
-#define LSBM_QUEUE_ITEM 1
-#endif
 constexpr uint32_t kQueueHeads = 8;
 constexpr uint32_t kQueueStride = LSBM_QUEUE_STRIDE;
 constexpr uint32_t kQueueWords = kQueueHeads * kQueueStride;
-constexpr uint32_t kQueueItem = LSBM_QUEUE_ITEM;  // fixed kernel: groups per queue item
 static_assert(kLdsBytes % 16 == 0 && kLdsBytes + 4u * kLdsKernelWords <= 160u * 1024u,
               "one LDS image per CU, plus the kernels' work counters");
 static_assert(kStreamHM % 16 == 0, "ds_read_b128 of a mask");

@@ -21,15 +21,27 @@ __shared__ uint32_t g_lds[kLdsWords];
 // share of a statically split batch tens of microseconds after the others,
 // while within one XCD all workgroups end within ~10 us
 // (tools/wave_spread_ragged.py).  No static split can
-// know which XCD is slow, so the items past the first row are handed out at
-// run time: one head word per XCC (kQueueHeads, each on its own 64-B line),
-// head x hands out items base + 8 j + x, j = 0, 1, ... (at any moment every
-// XCD streams the same window of the batch), and a wave whose head is
-// exhausted moves on to the next head, so the fast XCDs take the slow ones'
-// last items.  One returning device-scope atomicAdd per item, issued one
-// item ahead so that its latency (~1 us with every CU streaming) is hidden
-// behind the item's rows.  The heads are zeroed before each launch (stream-
-// ordered scratch, crc32c_engine.cc).
+// know which XCD is slow, so past the first row the work is handed out at run
+// time, in ITEMS of one group per wave of a workgroup:
+//   * global: one head word per XCC (kQueueHeads, kQueueStride words apart),
+//     head x hands out items 8 j + x, j = 0, 1, ... (every XCD streams the same
+//     window of the batch), and a workgroup whose head is exhausted moves on
+//     to the next head, so the fast XCDs take the slow ones' last items;
+//   * per workgroup (WgQueue): the waves take slots k = 0, 1, ... from an LDS
+//     counter; slot k is wave-group k % W of batch k / W, and batch b's item
+//     is claimed from the heads by the wave that took slot 0 of batch b - 1
+//     (kLead batches ahead) and published through an LDS ring of kRing
+//     entries.  One global atomic per W groups, so the returning atomic --
+//     ~5-7 us with every CU streaming, and retiring in order with the
+//     claiming wave's row loads -- stalls one wave in W once per batch
+//     (per-wave claims stalled every wave: 67-78% of HBM peak against 85%).
+// Protocol (checked exhaustively-by-sampling in tests/test_queue_schedule.py):
+// a workgroup's claims are made in batch order (publish(x) waits until batch
+// x - 1 is published), so an exhausted queue (kNone) is seen in order and
+// every claimed item is processed; entry x % kRing is reused only once all W
+// readers of batch x - kRing have read it.  No wait can form a cycle (each
+// waits only on smaller batches), and every spin is capped (kSpinCap): a
+// protocol fault gives wrong results, which the tests see, never a hang.
 // ---------------------------------------------------------------------------
 // (kQueueHeads, kQueueStride, kQueueWords: crc32c_types.h)
 
@@ -39,27 +51,84 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x & (kQueueHeads - 1);
 }
 
-// One claim from head h, issued by lane 0: the raw counter value (lane 0's
-// register; read it with readfirstlane when it is needed).
-__device__ __forceinline__ uint32_t queue_issue(uint32_t* heads, uint32_t h) {
+// One claim from head h by lane 0; wave-uniform result.
+__device__ __forceinline__ uint32_t queue_take(uint32_t* heads, uint32_t h) {
   uint32_t j = 0;
   if ((threadIdx.x & 63u) == 0) j = atomicAdd(heads + h * kQueueStride, 1u);
-  return j;
+  return __builtin_amdgcn_readfirstlane(j);
 }
 
-// Resolve a claim issued on head h: the item, or, when head h is exhausted,
-// claims from the next heads in turn (h moves with them: a head once found
-// exhausted stays so); `total` when every head is.  Items are base + 8 j + h.
-__device__ __forceinline__ uint64_t queue_resolve(uint32_t* heads, uint32_t& h, uint32_t pending, uint64_t base,
-                                                  uint64_t total, uint32_t& exhausted) {
-  uint64_t item = base + (uint64_t)__builtin_amdgcn_readfirstlane(pending) * kQueueHeads + h;
-  while (item >= total) {
-    if (++exhausted >= kQueueHeads) return total;
-    h = (h + 1) & (kQueueHeads - 1);
-    item = base + (uint64_t)__builtin_amdgcn_readfirstlane(queue_issue(heads, h)) * kQueueHeads + h;
+constexpr uint32_t kWqRing = 4, kWqLead = 1, kWqNone = 0xffffffffu, kSpinCap = 1u << 20;
+constexpr uint32_t kWqWords = 3 + 3 * kWqRing;  // next, head, exhausted, tag[R], item[R], read[R]
+static_assert(kWqLead == 1, "wave 0 publishes batch 1 only: the batches before the first slot-0 taker's");
+static_assert(kWqRing > kWqLead, "an entry is reused only after its batch's slots were all taken");
+
+// LDS words by address space: a generic (flat) pointer would make every
+// access a flat op, counted in vmcnt with the row loads (a spin would then
+// wait for all of them)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <uint32_t W>
+struct WgQueue {
+  uint32_t* heads;  // global heads
+  lds_u32* s;       // LDS words (kWqWords)
+  uint64_t items;   // items the heads hand out
+
+  __device__ __forceinline__ volatile lds_u32* v(uint32_t i) const { return (volatile lds_u32*)(s + i); }
+  // (thread 0, before a workgroup barrier)
+  __device__ __forceinline__ void init(uint32_t xcc) const {
+    *v(0) = W;  // slots 0 .. W-1: row 0, the waves' own
+    *v(1) = xcc;
+    *v(2) = 0;
+    for (uint32_t e = 0; e < kWqRing; e++) {
+      *v(3 + e) = 0;  // (tag 0: batch 0, which is never read)
+      *v(3 + kWqRing + e) = kWqNone;
+      *v(3 + 2 * kWqRing + e) = 0;
+    }
   }
-  return item;
-}
+  __device__ __forceinline__ uint32_t take() const {
+    uint32_t k = 0;
+    if ((threadIdx.x & 63u) == 0) k = __atomic_fetch_add(s, 1u, __ATOMIC_RELAXED);
+    return __builtin_amdgcn_readfirstlane(k);
+  }
+  __device__ __forceinline__ uint32_t rd(uint32_t i) const { return __builtin_amdgcn_readfirstlane(*v(i)); }
+  // Claim batch x's item from the heads and publish it (wave-uniform).
+  __device__ __forceinline__ void publish(uint32_t x) const {
+    const uint32_t e = x % kWqRing, pe = (x - 1) % kWqRing;
+    uint32_t spins = 0;
+    if (x >= 2)  // in batch order
+      while (rd(3 + pe) != x - 1 && ++spins < kSpinCap) __builtin_amdgcn_s_sleep(2);
+    if (x > kWqRing)  // the entry's previous batch read by all W
+      while (rd(3 + 2 * kWqRing + e) != W && ++spins < kSpinCap) __builtin_amdgcn_s_sleep(2);
+    uint32_t h = rd(1), out = rd(2), it = kWqNone;
+    while (spins < kSpinCap && out < kQueueHeads) {
+      const uint64_t cand = (uint64_t)queue_take(heads, h) * kQueueHeads + h;
+      if (cand < items) {
+        it = (uint32_t)cand;
+        break;
+      }
+      if (++out < kQueueHeads) h = (h + 1) & (kQueueHeads - 1);
+    }
+    if ((threadIdx.x & 63u) == 0) {  // (LDS ops of one wave complete in order: item before tag)
+      *v(1) = h;
+      *v(2) = out;
+      *v(3 + kWqRing + e) = it;
+      *v(3 + 2 * kWqRing + e) = 0;
+      *v(3 + e) = x;
+    }
+  }
+  // Batch b's item (kWqNone: the queue is exhausted), counted as read.
+  __device__ __forceinline__ uint32_t read(uint32_t b) const {
+    const uint32_t e = b % kWqRing;
+    uint32_t spins = 0;
+    while (rd(3 + e) != b)
+      if (++spins >= kSpinCap) return kWqNone;
+      else __builtin_amdgcn_s_sleep(2);
+    const uint32_t it = rd(3 + kWqRing + e);
+    if ((threadIdx.x & 63u) == 0) __atomic_fetch_add(s + 3 + 2 * kWqRing + e, 1u, __ATOMIC_RELAXED);
+    return it;
+  }
+};
 
 // Diagnostic builds only (-DLSBM_DIAG_STAMPS, tools/wave_spread.py): every
 // wave stamps its start (0), its first data (1) and its end (2) with
