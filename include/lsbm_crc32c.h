@@ -207,8 +207,9 @@ int lsbm_test_fail_host_pipeline(int chunks);
  * batch it takes.  Results are identical; for tests and A/B runs. */
 int lsbm_test_ragged_kernel(int which);
 
-/* Testing: the fixed-stride kernel's cross-XCC work queue on (1) or off (0,
- * the static interleave); -1 restores the default (LSBM_FIXED_QUEUE, on). */
+/* Testing / A/B: the fixed-stride kernel's cross-XCC work queue on (1) or off
+ * (0, the static interleave); -1 restores the default (LSBM_FIXED_QUEUE,
+ * off). */
 int lsbm_test_fixed_queue(int on);
 
 /* ---- host runtime (the C++ layers' sessions and worker pool) ---- */

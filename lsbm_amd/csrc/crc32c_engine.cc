@@ -230,16 +230,21 @@ uint64_t fixed_split_blocks() {
   return b;
 }
 
-// The fixed kernel's cross-XCC work queue (crc32c_units.h): LSBM_FIXED_QUEUE=0
-// keeps the static interleave (A/B).  Only for launches of at least 4 groups
-// per wave, and never while the stream is being captured into a graph (the
-// heads are per-call scratch).
+// The fixed kernel's cross-XCC work queue (crc32c_units.h WgQueue), OFF by
+// default (LSBM_FIXED_QUEUE=1 or lsbm_test_fixed_queue: on).  It does what it
+// is for -- the eight XCDs' waves end within 5% of the launch instead of 14%
+// but the chip's aggregate read rate does not move (config 2 84.8% either
+// way, config 3 +0.7 points, a 10M-block shard -1 point; DESIGN.md section
+// 4): a statically split batch's fast XCDs finish early and the slow ones
+// then get their bandwidth.  Only for launches of at least 4 groups per wave,
+// and never while the stream is being captured into a graph (the heads are
+// per-call scratch).
 std::atomic<int> g_fixed_queue{-1};  // -1: not read yet; 0 off, 1 on (lsbm_test_fixed_queue)
 bool fixed_queue_on() {
   int q = g_fixed_queue.load(std::memory_order_relaxed);
   if (q < 0) {
     const char* v = getenv("LSBM_FIXED_QUEUE");
-    q = (v && v[0] == '0') ? 0 : 1;
+    q = (v && v[0] == '1') ? 1 : 0;
     int expect = -1;
     if (!g_fixed_queue.compare_exchange_strong(expect, q)) q = expect;
   }
