@@ -309,6 +309,15 @@ int run_ragged_one(RaggedArgs a, hipStream_t stream) {
       bounds = nullptr;
     }
   }
+  // SSTable trailer batches (verify, dense trailer CRCs; not the fused seal,
+  // whose trailer epilogue walks the wave's one range): equal-count pieces of
+  // kSstPieceBlocks blocks, claimed by the workgroup's waves in turn
+  // (crc32c_units.h next_piece), no bounds table.
+  if (!bounds && a.extents == kExtHandles && (a.mode == kModeSstVerify || (a.mode == kModeSstCrc && !a.file)) &&
+      a.n < 0xffffffffull) {
+    const uint64_t per_wave = a.n / ((uint64_t)kSstPieceBlocks * nwaves);
+    if (per_wave >= 2) a.nchunks = per_wave;
+  }
   const hipError_t e = launch_ragged(a, (int)st->num_cus, stream);
   if (bounds) (void)hipFreeAsync(bounds, stream);
   return e == hipSuccess ? LSBM_OK : fail_hip(e, "crc32c_units_kernel");

@@ -136,11 +136,15 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
   uint64_t b_lo, b_hi;
   DIAG_STAMP_W(0, wave);
   wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
-  const uint32_t* __restrict__ bnd = args.bounds;
-  if (chunked) {
-    b_lo = bnd[pi];
-    b_hi = bnd[pi + 1];
-  }
+  if (chunked) piece_range(args, pi, p_end, b_lo, b_hi);
+  // a chunked sweep's later pieces are claimed from an LDS counter
+  // (next_piece, crc32c_units.h), also by the units walk it may fall back to
+  __shared__ uint32_t s_claim;
+  lds_u32* claim = nullptr;
+#ifndef LSBM_PIECES_STATIC
+  if (chunked) claim = (lds_u32*)&s_claim;
+  if (threadIdx.x == 0) s_claim = kStreamWavesPerWg;  // (ordered by load_lds_tables' barrier)
+#endif
   load_lds_tables<kStreamThreads>(g_lds, dc);
   DIAG_STAMP_W(1, wave);
   const uint64_t base = reinterpret_cast<uint64_t>(args.base);
@@ -662,10 +666,9 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
       b0 += nb;
     }
     if (!chunked || resume != ~0ull) break;
-    pi += (uint32_t)nwaves;
+    pi = claim ? next_piece<kStreamWavesPerWg>(claim, pi, nwaves) : pi + (uint32_t)nwaves;
     if (pi >= p_end) break;
-    b_lo = bnd[pi];
-    b_hi = bnd[pi + 1];
+    piece_range(args, pi, p_end, b_lo, b_hi);
   }
 #ifdef LSBM_STREAM_STATS
   if (lane == 0u)
@@ -678,7 +681,8 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     // The units walk from block `resume` on: the rest of this range, then (a
     // chunked sweep) this wave's range of every later chunk.  Its bad blocks
     // are counted by the walk; this wave's nbad holds the streamed ones.
-    units_walk<kFallbackRows, kMode, kExt>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end, false, resume);
+    units_walk<kFallbackRows, kMode, kExt, kStreamWavesPerWg>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end,
+                                                              false, resume, claim);
   }
   if constexpr (kMode == kModeLogSeal) {
     // Deferred headers: this wave's masked CRCs went densely to out[] with

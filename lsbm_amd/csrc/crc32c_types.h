@@ -148,6 +148,11 @@ constexpr uint32_t kChunkBlocks = LSBM_CHUNK_BLOCKS;
 constexpr uint32_t kMinChunks = 8;
 constexpr uint32_t kUnitRows = 48;  // A/B 24..96 rows: plateau from 48
 constexpr uint32_t kSstUnitRows = 40;  // SSTable trailer modes: a ~4 KiB block is one unit
+#ifndef LSBM_SST_PIECE_BLOCKS  // (A/B builds override)
+#define LSBM_SST_PIECE_BLOCKS 16
+#endif
+// SSTable trailer batches: blocks per claimed piece (two 8-block rounds)
+constexpr uint32_t kSstPieceBlocks = LSBM_SST_PIECE_BLOCKS;
 
 struct RaggedArgs {
   const uint8_t* base;      // extents are byte offsets from here

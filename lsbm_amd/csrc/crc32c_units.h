@@ -485,13 +485,18 @@ __global__ __launch_bounds__(256) void range_bounds_kernel(RaggedArgs args, uint
 // chunked: piece index pi = c * nwaves + w of the range being walked, and
 // p_end the end of the pieces (nchunks * nwaves < 2^32); the chunked walk
 // reads its ranges from args.bounds itself (b_lo / b_hi unset).
+// SSTable modes over a handle batch: equal-count pieces (piece_range), no
+// bounds table -- their blocks are near-uniform (one unit each).
+template <uint32_t kMode, uint32_t kExt>
+constexpr bool kArithPieces = (kMode == kModeSstVerify || kMode == kModeSstCrc) && kExt == kExtHandles;
+
 template <uint32_t kMode, uint32_t kExt>
 __device__ __forceinline__ void wave_range(const RaggedArgs& args, uint64_t wave, uint64_t nwaves,
                                            bool& chunked, uint32_t& pi, uint32_t& p_end,
                                            uint64_t& b_lo, uint64_t& b_hi) {
   constexpr bool kChunkable = (kMode == kModeOut || kMode == kModeVerify) &&
                               (kExt == kExtOffsets || kExt == kExtHandles);
-  chunked = kChunkable && args.bounds != nullptr;
+  chunked = (kChunkable && args.bounds != nullptr) || (kArithPieces<kMode, kExt> && args.nchunks != 0);
   pi = (uint32_t)wave;
   p_end = (uint32_t)(args.nchunks * nwaves);
   b_lo = args.n * wave / nwaves;
@@ -508,6 +513,42 @@ __device__ __forceinline__ void wave_range(const RaggedArgs& args, uint64_t wave
   }
 }
 
+// Piece i of a chunked sweep: [bounds[i], bounds[i + 1]) from the bounds
+// table, or, without one (kArithPieces), the equal-count cut of the batch
+// into P = nchunks * nwaves pieces.
+__device__ __forceinline__ void piece_range(const RaggedArgs& a, uint32_t i, uint32_t P, uint64_t& lo,
+                                            uint64_t& hi) {
+  if (a.bounds) {
+    lo = a.bounds[i];
+    hi = a.bounds[i + 1];
+  } else {
+    lo = a.n * i / P;
+    hi = a.n * (i + 1) / P;
+  }
+}
+
+// Which piece a wave walks next.  Static (LSBM_PIECES_STATIC, A/B): its own
+// range of the next chunk, pi + nwaves.  Default (round 6): the workgroup's
+// waves take their pieces in turn from an LDS counter -- the fixed kernel's
+// round-5 schedule -- so a fast wave takes more of them: slot k of the
+// workgroup is piece (k / W) nwaves + W blockIdx + k % W (the static sweep's
+// pieces of this workgroup; each wave's first piece is its own, k = W is the
+// first claim).  (On units and stream kernels the static split left the
+// waves of one workgroup ending up to ~100 us apart on a 0.65 ms launch:
+// tools/wave_spread_ragged.py)
+template <uint32_t W>
+__device__ __forceinline__ uint32_t next_piece(lds_u32* claim, uint32_t pi, uint64_t nwaves) {
+#ifndef LSBM_PIECES_STATIC
+  if (claim) {
+    uint32_t k = 0;
+    if ((threadIdx.x & 63u) == 0) k = __atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED);
+    k = __builtin_amdgcn_readfirstlane(k);
+    return (k / W) * (uint32_t)nwaves + blockIdx.x * W + k % W;
+  }
+#endif
+  return pi + (uint32_t)nwaves;
+}
+
 // The units walk: the blocks [b_lo, b_hi) (or, chunked, this wave's range of
 // every chunk) in rounds of 8 units.  crc32c_units_kernel runs it over the
 // wave's range; crc32c_stream_kernel runs it over a sub-piece whose extents
@@ -516,11 +557,11 @@ __device__ __forceinline__ void wave_range(const RaggedArgs& args, uint64_t wave
 // first_lo: the walk starts at block first_lo (>= the range's start) of its
 // first range; the stream kernel resumes there after streaming the blocks
 // before it (chunked too: later ranges are walked whole).
-template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt, uint32_t kW = kWavesPerWg>
 __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave, const uint64_t nwaves,
                                            uint64_t b_lo, uint64_t b_hi, const bool chunked,
                                            uint32_t pi, const uint32_t p_end, const bool load_tables,
-                                           const uint64_t first_lo = 0) {
+                                           const uint64_t first_lo = 0, lds_u32* claim = nullptr) {
   args.mode = kMode;   // compile-time: lets the compiler drop the other modes' code
   args.extents = kExt;
   const DevConsts* __restrict__ dc = args.dc;
@@ -529,21 +570,55 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
   const uint32_t lb = row_lane_base(lane);
   const uint32_t L0 = lb | kRowTab[0], L1 = lb | kRowTab[1], L2 = lb | kRowTab[2], L3 = lb | kRowTab[3];
   const uint32_t lane_fin = kNibFin | lb;
-  const uint32_t* __restrict__ bnd = args.bounds;
+  // Static pieces: the next chunk's range is loaded a chunk ahead (pf_*).
+  // Claimed pieces (claim != null): the next piece is claimed when this one
+  // ends -- a claim made ahead would hold the wave to it -- and its bounds
+  // loaded then (equal-count pieces need no load).
+  uint32_t pf_lo = 0, pf_hi = 0;
+  bool pf = false;  // pf_* hold piece pi + nwaves
+  auto piece = [&](uint32_t i, uint64_t& lo, uint64_t& hi) { piece_range(args, i, p_end, lo, hi); };
+  // the next non-empty piece after pi into (pi, lo, hi); false: none left
+  auto advance = [&](uint64_t& lo, uint64_t& hi) -> bool {
+    for (;;) {
+      const uint32_t np = claim ? next_piece<kW>(claim, pi, nwaves) : pi + (uint32_t)nwaves;
+      if (np >= p_end) return false;
+      if (!claim && pf && np == pi + (uint32_t)nwaves) {
+        lo = pf_lo;
+        hi = pf_hi;
+      } else {
+        piece(np, lo, hi);
+      }
+      pi = np;
+      pf = false;
+      if (lo < hi) break;
+    }
 #ifndef LSBM_NO_BOUNDS_PREFETCH  // A/B builds only
-  uint32_t pf_lo = 0, pf_hi = 0;  // the next chunk's range, loaded a chunk ahead
+    if (!claim && pi + nwaves < p_end) {
+      uint64_t l2, h2;
+      piece(pi + (uint32_t)nwaves, l2, h2);
+      pf_lo = (uint32_t)l2;
+      pf_hi = (uint32_t)h2;
+      pf = true;
+    }
 #endif
-  auto piece = [&](uint32_t i, auto& lo, auto& hi) {  // i < p_end
-    lo = bnd[i];
-    hi = bnd[i + 1];
+    return true;
   };
   if (chunked) {
     piece(pi, b_lo, b_hi);
     b_lo = b_lo < first_lo ? first_lo : b_lo;
-    while (b_lo >= b_hi && pi + nwaves < p_end) piece(pi += (uint32_t)nwaves, b_lo, b_hi);  // (empty)
+    if (b_lo >= b_hi) {
+      if (!advance(b_lo, b_hi)) b_lo = b_hi;  // (nothing left: an empty walk)
+    } else {
 #ifndef LSBM_NO_BOUNDS_PREFETCH
-    if (pi + nwaves < p_end) piece(pi + (uint32_t)nwaves, pf_lo, pf_hi);
+      if (!claim && pi + nwaves < p_end) {
+        uint64_t l2, h2;
+        piece(pi + (uint32_t)nwaves, l2, h2);
+        pf_lo = (uint32_t)l2;
+        pf_hi = (uint32_t)h2;
+        pf = true;
+      }
 #endif
+    }
   }
   const uint64_t dummy = reinterpret_cast<uint64_t>(dc->zero16);
   const uint32_t* __restrict__ init = args.init;
@@ -771,22 +846,8 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
     uint64_t nb = cur_b + jnext;
     uint32_t no = cur_o + 8 - pre8;
     uint64_t next_hi = range_hi;
-    if (chunked && nb >= range_hi) {  // (wave-uniform) this range is done: the next chunk's
-      if (pi + nwaves < p_end) {
-        pi += (uint32_t)nwaves;
-#ifndef LSBM_NO_BOUNDS_PREFETCH
-        nb = pf_lo;
-        next_hi = pf_hi;
-#else
-        piece(pi, nb, next_hi);
-#endif
-        while (nb >= next_hi && pi + nwaves < p_end) piece(pi += (uint32_t)nwaves, nb, next_hi);
-#ifndef LSBM_NO_BOUNDS_PREFETCH
-        if (pi + nwaves < p_end) piece(pi + (uint32_t)nwaves, pf_lo, pf_hi);
-#endif
-      } else {
-        nb = next_hi = range_hi;  // (the last chunk: done)
-      }
+    if (chunked && nb >= range_hi) {  // (wave-uniform) this range is done: the next piece's
+      if (!advance(nb, next_hi)) nb = next_hi = range_hi;  // (none left: done)
       no = 0;
     }
     ExtRaw rn;

@@ -1272,6 +1272,55 @@ def test_host_staged_multi_device_shards(torch_cuda, oracle):
         assert np.array_equal(got, oracle.batch_offsets(data, offs, init, masked=True)), devs
 
 
+@pytest.mark.parametrize("order", ["sorted", "shuffled"])
+def test_sst_claimed_pieces_ragged_sizes(torch_cuda, oracle, order):
+    """SSTable verify and dense trailer CRCs over >= 131,072 handles go as
+    equal-count pieces claimed in turn by a workgroup's waves (crc32c_units.h
+    next_piece; round 6).  Here 300,001 blocks of 0-9,000 B (so the pieces are
+    far from equal in bytes), handles in file order or shuffled, a few past
+    the image: every trailer CRC equals the oracle's WriteRawBlock CRC, every
+    verify flag is right, and the bad handles are counted exactly."""
+    torch = torch_cuda
+    from lsbm_amd import table
+    rng = np.random.default_rng(21)
+    n = 300_001
+    sizes = rng.integers(0, 9001, n)
+    sizes[::101] = 0
+    handles, total = table.layout_blocks(sizes)
+    handles = handles.astype(np.int64).copy()
+    bad = set(rng.choice(n, 7, replace=False).tolist())
+    for i in bad:
+        handles[2 * i] = total + 1 + i  # past the image: "truncated block read"
+    types = rng.integers(0, 2, n).astype(np.uint8)
+    perm = np.arange(n) if order == "sorted" else rng.permutation(n)
+    h2 = handles.reshape(n, 2)[perm].reshape(-1).copy()
+    t2 = types[perm]
+    d = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    engine_fill(d, 0x5EED0021)
+    img = d.cpu().numpy()[:total]
+    good = np.array([p not in bad for p in perm])
+    want = np.zeros(n, dtype=np.uint32)
+    want[good] = oracle.sst_trailers_mt(img, 0, h2.reshape(n, 2)[good].reshape(-1).astype(np.uint64), t2[good])
+    dh = _dev(torch, h2)
+    tc, nb = table.trailer_crcs(d, dh, _dev(torch, t2))
+    assert int(nb.item()) == len(bad)
+    assert np.array_equal(_u32(tc), want)
+    # seal (the fused seal, static ranges) then verify (claimed pieces)
+    nbad = table.seal_blocks(d, dh, _dev(torch, t2))
+    assert int(nbad.item()) == len(bad)
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == len(bad)
+    okh = ok.cpu().numpy()
+    assert np.array_equal(okh != 0, good)
+    # one corrupted payload byte in a block of each half
+    hi = [i for i in (n // 4, 3 * n // 4) if good[i] and h2[2 * i + 1] > 0]
+    for i in hi:
+        d[int(h2[2 * i]) + int(h2[2 * i + 1]) // 2] ^= 0x40
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == len(bad) + len(hi)
+    assert set(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == set(np.nonzero(~good)[0].tolist()) | set(hi)
+
+
 def test_sst_handles_past_the_image_merged_seal(torch_cuda, oracle):
     """The same "truncated block read" handles (table/format.cc:88-91) at
     >= 131,072 blocks, where lsbm_sst_seal_dev computes the CRCs densely and
