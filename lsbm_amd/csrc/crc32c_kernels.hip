@@ -286,19 +286,24 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   uint64_t b_lo, b_hi;
   DIAG_STAMP(0);
   wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
+  DIAG_STAMP(1);
+#ifndef LSBM_PIECES_STATIC
   // a chunked sweep's pieces are claimed from an LDS counter (next_piece);
   // the walk claims before its table fill's barrier, hence one of its own
-  __shared__ uint32_t s_claim;
-  lds_u32* claim = nullptr;
-#ifndef LSBM_PIECES_STATIC
-  if (chunked) {
-    if (threadIdx.x == 0) s_claim = kWavesPerWg;
-    claim = (lds_u32*)&s_claim;
-  }
-  if (__builtin_amdgcn_readfirstlane((uint32_t)chunked)) __syncthreads();  // (chunked: wave-uniform, grid-uniform)
+  // (chunked is grid-uniform)
+  if constexpr (kCanChunk<kMode, kExt>) {
+    if (chunked) {
+      __shared__ uint32_t s_claim;
+      if (threadIdx.x == 0) s_claim = kWavesPerWg;
+      __syncthreads();
+      units_walk<kMaxRows, kMode, kExt, true>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true, 0,
+                                              (lds_u32*)&s_claim);
+    } else {
+      units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
+    }
+  } else
 #endif
-  DIAG_STAMP(1);
-  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true, 0, claim);
+  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
   if constexpr (kMode == kModeSstCrc && kExt == kExtHandles) {
     if (args.file != nullptr) {  // (SstCrc is never chunked: [b_lo, b_hi) is this wave's range)
       // this wave's out[] stores complete (s_waitcnt vmcnt(0)) before it reads

@@ -681,8 +681,15 @@ __global__ __launch_bounds__(kStreamThreads) void crc32c_stream_kernel(RaggedArg
     // The units walk from block `resume` on: the rest of this range, then (a
     // chunked sweep) this wave's range of every later chunk.  Its bad blocks
     // are counted by the walk; this wave's nbad holds the streamed ones.
-    units_walk<kFallbackRows, kMode, kExt, kStreamWavesPerWg>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end,
-                                                              false, resume, claim);
+    if constexpr (kCanChunk<kMode, kExt>) {
+      if (claim)
+        units_walk<kFallbackRows, kMode, kExt, true, kStreamWavesPerWg>(args, wave, nwaves, resume, b_hi, chunked, pi,
+                                                                        p_end, false, resume, claim);
+      else
+        units_walk<kFallbackRows, kMode, kExt>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end, false, resume);
+    } else {
+      units_walk<kFallbackRows, kMode, kExt>(args, wave, nwaves, resume, b_hi, chunked, pi, p_end, false, resume);
+    }
   }
   if constexpr (kMode == kModeLogSeal) {
     // Deferred headers: this wave's masked CRCs went densely to out[] with

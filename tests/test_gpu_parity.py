@@ -1305,6 +1305,10 @@ def test_sst_claimed_pieces_ragged_sizes(torch_cuda, oracle, order):
     tc, nb = table.trailer_crcs(d, dh, _dev(torch, t2))
     assert int(nb.item()) == len(bad)
     assert np.array_equal(_u32(tc), want)
+    # the image is not sealed yet: every block fails verify (and is counted:
+    # per lane, one atomic per walk)
+    ok, nb = table.verify_blocks(d, dh)
+    assert int(nb.item()) == n and not bool(ok.any())
     # seal (the fused seal, static ranges) then verify (claimed pieces)
     nbad = table.seal_blocks(d, dh, _dev(torch, t2))
     assert int(nbad.item()) == len(bad)
