@@ -263,7 +263,7 @@ struct Job {
 // two sees the other: no lost wake-up).
 // Round 4: with a mutex round trip per piece a parallel_for cost ~50 us; with
 // one per worker and job (pick and drop), 25-37 us of empty pieces on 16
-// threads (tools/ab/r4/pool_overhead.py).
+// threads (round 4; docs/DESIGN_HISTORY.md section 6).
 class WorkPool {
  public:
   static constexpr int kJobSlots = 64;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One parameterised A/B runner (replaces round 4's 30 tools/ab/r4/checkN.sh):
+# One parameterised A/B runner (replaces round 4's 30 one-off check scripts):
 # for each variant, an optional GPU test step, then PASSES interleaved passes
 # of a bench command over all variants, each run under its own time limit;
 # the first failing step ends the script (no retries: DESIGN/CLAUDE GPU rules).

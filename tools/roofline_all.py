@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One device entry point per process, for rocprofv3 (tools/r5/roofline.sh).
+"""One device entry point per process, for rocprofv3 (tools/roofline.sh).
 
     python tools/roofline_all.py ENTRY
 
@@ -9,7 +9,7 @@ sampled results against the oracle, and prints ONE JSON line naming the
 entry, its kernel (a regex over rocprof kernel names) and its ALGORITHMIC
 bytes per launch.  Run under `rocprofv3 --kernel-trace --stats`, the kernel's
 average duration comes from rocprof itself, not from HIP events; under a
-`--pmc FETCH_SIZE` pass, its HBM bytes.  tools/r5/roofline_summary.py joins
+`--pmc FETCH_SIZE` pass, its HBM bytes.  tools/roofline_summary.py joins
 the three.
 
   fixed4k     config 2: 1M x 4096 B, lsbm_crc32c_fixed_dev        (block bytes)
