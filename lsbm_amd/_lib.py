@@ -109,6 +109,8 @@ def lib():
                 "There is no CPU fallback.")
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("LSBM_LIB_PATH") and not hasattr(handle, name):
+                continue  # (an older build for an A/B: only the symbols it has)
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -3,7 +3,7 @@
 # (tests/test_gpu_parity.py::test_db_bench_gpu_tables), then the three builds
 # interleaved (tools/db_bench_ab.py).  Output under gpurun_out/dbbench/.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/dbbench; mkdir -p $OUT
 nproc > $OUT/host.txt; lscpu | grep "Model name" >> $OUT/host.txt
 timeout -k 10 300 python -u -m pytest -x -v -s --timeout 280 --timeout-method thread \

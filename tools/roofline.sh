@@ -6,7 +6,7 @@
 # The per-dispatch counter CSVs are summarised and deleted as they go (gpurun
 # copies back at most 64 MiB).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/roofline}
 mkdir -p $OUT
