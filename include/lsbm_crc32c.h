@@ -211,6 +211,10 @@ int lsbm_test_ragged_kernel(int which);
  * (0, the static interleave); -1 restores the default (LSBM_FIXED_QUEUE,
  * off). */
 int lsbm_test_fixed_queue(int on);
+/* Testing / A/B: SSTable trailer batches (verify, dense trailer CRCs) as
+ * equal-count pieces claimed by a workgroup's waves (1) or one range per wave
+ * (0); -1 restores the default (LSBM_SST_PIECES, pieces). */
+int lsbm_test_sst_pieces(int on);
 
 /* ---- host runtime (the C++ layers' sessions and worker pool) ---- */
 /* Worker threads of the host pool: usable cores - 1, where usable cores = the

@@ -54,6 +54,7 @@ SIGNATURES = {
     "lsbm_test_fail_host_pipeline": (_int, [_int]),
     "lsbm_test_ragged_kernel": (_int, [_int]),
     "lsbm_test_fixed_queue": (_int, [_int]),
+    "lsbm_test_sst_pieces": (_int, [_int]),
     "lsbm_host_threads": (_int, []),
     "lsbm_host_register": (_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "lsbm_host_unregister": (_int, [ctypes.c_void_p]),

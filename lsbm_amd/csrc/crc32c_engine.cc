@@ -251,6 +251,20 @@ bool fixed_queue_on() {
   return q == 1;
 }
 
+// SSTable trailer batches as claimed equal-count pieces (default) or one range
+// per wave (LSBM_SST_PIECES=0, lsbm_test_sst_pieces: A/B runs).
+std::atomic<int> g_sst_pieces{-1};  // -1: not read yet
+bool sst_pieces_on() {
+  int q = g_sst_pieces.load(std::memory_order_relaxed);
+  if (q < 0) {
+    const char* v = getenv("LSBM_SST_PIECES");
+    q = (v && v[0] == '0') ? 0 : 1;
+    int expect = -1;
+    if (!g_sst_pieces.compare_exchange_strong(expect, q)) q = expect;
+  }
+  return q == 1;
+}
+
 int grid_for(const DeviceState* st, uint64_t n_blocks) {
   const uint64_t groups = (n_blocks + 7) / 8;
   const uint64_t wgs = (groups + kWavesPerWg - 1) / kWavesPerWg;
@@ -280,6 +294,7 @@ int run_ragged_one(RaggedArgs a, hipStream_t stream) {
   a.u_noinit = u_noinit();
   a.bounds = nullptr;
   a.nchunks = 0;
+  a.piece_q = a.piece_r = 0;
   const uint64_t nwaves =
       (uint64_t)st->num_cus * (ragged_uses_stream(a) ? kStreamWavesPerWg : kWavesPerWg);
   // (LSBM_SWEEP_CHUNK_BLOCKS: A/B runs only; 0 = no chunked sweep)
@@ -313,10 +328,15 @@ int run_ragged_one(RaggedArgs a, hipStream_t stream) {
   // whose trailer epilogue walks the wave's one range): equal-count pieces of
   // kSstPieceBlocks blocks, claimed by the workgroup's waves in turn
   // (crc32c_units.h next_piece), no bounds table.
-  if (!bounds && a.extents == kExtHandles && (a.mode == kModeSstVerify || (a.mode == kModeSstCrc && !a.file)) &&
-      a.n < 0xffffffffull) {
+  if (sst_pieces_on() && !bounds && a.extents == kExtHandles &&
+      (a.mode == kModeSstVerify || (a.mode == kModeSstCrc && !a.file)) && a.n < 0xffffffffull) {
     const uint64_t per_wave = a.n / ((uint64_t)kSstPieceBlocks * nwaves);
-    if (per_wave >= 2) a.nchunks = per_wave;
+    if (per_wave >= 2) {
+      const uint64_t P = per_wave * nwaves;
+      a.nchunks = per_wave;
+      a.piece_q = (uint32_t)(a.n / P);
+      a.piece_r = (uint32_t)(a.n % P);
+    }
   }
   const hipError_t e = launch_ragged(a, (int)st->num_cus, stream);
   if (bounds) (void)hipFreeAsync(bounds, stream);
@@ -354,6 +374,14 @@ int run_ragged(RaggedArgs a, hipStream_t stream) {
 extern "C" __attribute__((visibility("default"))) int lsbm_test_fixed_queue(int on) {
   if (on < -1 || on > 1) return -1;
   g_fixed_queue.store(on);
+  return 0;
+}
+
+// Testing (include/lsbm_crc32c.h): SSTable trailer pieces on (1) or off (0);
+// -1 back to LSBM_SST_PIECES's default.
+extern "C" __attribute__((visibility("default"))) int lsbm_test_sst_pieces(int on) {
+  if (on < -1 || on > 1) return -1;
+  g_sst_pieces.store(on);
   return 0;
 }
 

@@ -276,7 +276,12 @@ __global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restric
 // wave's last row load (none of them queues in front of its reads) and
 // overlap the other waves' streaming, instead of a second pass over the
 // trailers after the kernel.
-template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt>
+// kPieces (launch_ragged: a chunked sweep, or SSTable trailer pieces): the
+// walk over pieces; otherwise the walk of one range, compiled without the
+// piece code.  Two kernels rather than two walks in one: with both inlined
+// the one-range walks (the fused seal's among them) ran 1.3-2 points slower
+// than round 5's single-walk kernel on the same box (profiles/r06/events_ab/).
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt, bool kPieces>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs args) {
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerWg +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -287,23 +292,22 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
   DIAG_STAMP(0);
   wave_range<kMode, kExt>(args, wave, nwaves, chunked, pi, p_end, b_lo, b_hi);
   DIAG_STAMP(1);
+  if constexpr (kPieces) {
 #ifndef LSBM_PIECES_STATIC
-  // a chunked sweep's pieces are claimed from an LDS counter (next_piece);
-  // the walk claims before its table fill's barrier, hence one of its own
-  // (chunked is grid-uniform)
-  if constexpr (kCanChunk<kMode, kExt>) {
-    if (chunked) {
-      __shared__ uint32_t s_claim;
-      if (threadIdx.x == 0) s_claim = kWavesPerWg;
-      __syncthreads();
-      units_walk<kMaxRows, kMode, kExt, true>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true, 0,
-                                              (lds_u32*)&s_claim);
-    } else {
-      units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
-    }
-  } else
+    // the pieces are claimed from an LDS counter (next_piece); the walk claims
+    // before its table fill's barrier, hence one of its own
+    __shared__ uint32_t s_claim;
+    if (threadIdx.x == 0) s_claim = kWavesPerWg;
+    __syncthreads();
+    units_walk<kMaxRows, kMode, kExt, true>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true, 0,
+                                            (lds_u32*)&s_claim);
+#else
+    units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
 #endif
-  units_walk<kMaxRows, kMode, kExt>(args, wave, nwaves, b_lo, b_hi, chunked, pi, p_end, true);
+  } else {
+    units_walk<kMaxRows, kMode, kExt, false, kWavesPerWg, false>(args, wave, nwaves, b_lo, b_hi, false, pi, p_end,
+                                                                true);
+  }
   if constexpr (kMode == kModeSstCrc && kExt == kExtHandles) {
     if (args.file != nullptr) {  // (SstCrc is never chunked: [b_lo, b_hi) is this wave's range)
       // this wave's out[] stores complete (s_waitcnt vmcnt(0)) before it reads
@@ -489,13 +493,25 @@ int set_ragged_policy(int p) {
   return 0;
 }
 
+// The units kernel for a's schedule: over pieces when the engine set a chunked
+// sweep (bounds) or SSTable trailer pieces (nchunks), wave_range's `chunked`.
+template <uint32_t R, uint32_t M, uint32_t X>
+void launch_units(const RaggedArgs& a, int grid, hipStream_t stream) {
+  if constexpr (kCanChunk<M, X>) {
+    if (a.bounds != nullptr || a.nchunks != 0) {
+      hipLaunchKernelGGL((crc32c_units_kernel<R, M, X, true>), dim3(grid), dim3(kBlockThreads), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((crc32c_units_kernel<R, M, X, false>), dim3(grid), dim3(kBlockThreads), 0, stream, a);
+}
+
 // grid: one workgroup per CU (the LDS image); the waves per workgroup differ
 // (kWavesPerWg, kStreamWavesPerWg), and a chunked sweep's bounds (a.bounds)
 // must have been computed for the kernel's wave count.
 hipError_t launch_ragged(const RaggedArgs& a, int grid, hipStream_t stream) {
   if (ragged_uses_stream(a)) return launch_stream(a, grid, stream);
-#define LSBM_LAUNCH_UNITS(R, M, X) \
-  hipLaunchKernelGGL((crc32c_units_kernel<R, M, X>), dim3(grid), dim3(kBlockThreads), 0, stream, a)
+#define LSBM_LAUNCH_UNITS(R, M, X) launch_units<R, M, X>(a, grid, stream)
   switch (a.mode) {
     case kModeOut:
       if (a.extents == kExtOffsets) LSBM_LAUNCH_UNITS(LSBM_UNIT_ROWS, kModeOut, kExtOffsets);

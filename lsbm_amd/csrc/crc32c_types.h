@@ -179,6 +179,10 @@ struct RaggedArgs {
   // c < nchunks, from range_bounds_kernel; null: one range per wave.
   const uint32_t* bounds;
   uint64_t nchunks;
+  // Equal-count pieces (no bounds table): piece i is [i q + min(i, r), + q +
+  // (i < r)) with q = n / P, r = n % P, P = nchunks * nwaves (set by the host:
+  // no 64-bit division on the device).
+  uint32_t piece_q, piece_r;
 };
 
 }  // namespace lsbm

@@ -519,15 +519,16 @@ __device__ __forceinline__ void wave_range(const RaggedArgs& args, uint64_t wave
 
 // Piece i of a chunked sweep: [bounds[i], bounds[i + 1]) from the bounds
 // table, or, without one (kArithPieces), the equal-count cut of the batch
-// into P = nchunks * nwaves pieces.
+// into P = nchunks * nwaves pieces (RaggedArgs piece_q, piece_r).
 __device__ __forceinline__ void piece_range(const RaggedArgs& a, uint32_t i, uint32_t P, uint64_t& lo,
                                             uint64_t& hi) {
   if (a.bounds) {
     lo = a.bounds[i];
     hi = a.bounds[i + 1];
   } else {
-    lo = a.n * i / P;
-    hi = a.n * (i + 1) / P;
+    (void)P;
+    lo = (uint64_t)i * a.piece_q + (i < a.piece_r ? i : a.piece_r);
+    hi = lo + a.piece_q + (i < a.piece_r ? 1u : 0u);
   }
 }
 
@@ -562,12 +563,17 @@ __device__ __forceinline__ uint32_t next_piece(lds_u32* claim, uint32_t pi, uint
 // first range; the stream kernel resumes there after streaming the blocks
 // before it (chunked too: later ranges are walked whole).
 // kClaim: the walk's pieces are claimed (claim, next_piece) -- a compile-time
-// switch, so that the walks that never claim keep their registers.
-template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt, bool kClaim = false, uint32_t kW = kWavesPerWg>
+// switch, so that the walks that never claim keep their registers; kChunks
+// false: a walk of one range (chunked_in is false), compiled without the
+// piece code (the SSTable walks run at 128 VGPRs: the dead piece state cost
+// their one-range walks, the fused seal's, 1.3 points).
+template <uint32_t kMaxRows, uint32_t kMode, uint32_t kExt, bool kClaim = false, uint32_t kW = kWavesPerWg,
+          bool kChunks = true>
 __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave, const uint64_t nwaves,
-                                           uint64_t b_lo, uint64_t b_hi, const bool chunked,
+                                           uint64_t b_lo, uint64_t b_hi, const bool chunked_in,
                                            uint32_t pi, const uint32_t p_end, const bool load_tables,
                                            const uint64_t first_lo = 0, lds_u32* claim_arg = nullptr) {
+  const bool chunked = kChunks && chunked_in;
   lds_u32* const claim = kClaim ? claim_arg : nullptr;
   args.mode = kMode;   // compile-time: lets the compiler drop the other modes' code
   args.extents = kExt;
@@ -665,10 +671,12 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
   uint64_t pend_a = 0;  // this lane's parked result (0 = none), see retire()
   uint32_t pend_v = 0, pend_i = 0;
   uint32_t round = 0;   // rounds retired so far (wave-uniform)
-  // Bad records are counted per lane and added to *nbad once per walk: one
+  // Bad records are counted wave-uniform (one ballot per round, in converged
+  // code, so the count lives in an SGPR) and added to *nbad once per walk: one
   // atomic per bad block on one address serialises at the memory side (a
-  // batch of 1M bad blocks took 8.7 ms instead of 0.65, round 6).
-  uint32_t nbad_l = 0;
+  // batch of 1M bad blocks took 8.7 ms instead of 0.65), and a per-lane count
+  // was one VGPR too many -- the SSTable walks spilled (round 6).
+  uint32_t nbad_w = 0;
   auto retire = [&]() {
     const uint32_t raw = merge_braids(g_lds, p0, p1, p2, p3, lane_fin);
     uint32_t v = raw;
@@ -694,6 +702,21 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
     // finish: register after the block = A^-z(v) (A^(1-z) for the seal's type byte)
     const uint32_t l = cols_apply(pfin, v, li);
     const uint32_t crc = l ^ 0xffffffffu;
+    // this round's bad records (a group's lanes agree; lane 0 of the group counts)
+    bool good = true;
+    if constexpr (mode == kModeSstSeal || mode == kModeSstCrc || mode == kModeLogSeal) {
+      good = pfits;
+    } else if constexpr (mode == kModeVerify) {
+      good = ((args.flags & 1u) ? mask_crc(crc) : crc) == paux0;
+    } else if constexpr (mode != kModeOut) {  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
+#ifndef LSBM_VERIFY_TWO_LOADS
+      good = pfits && unmask_crc(paux0) == crc;
+#else
+      good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
+#endif
+    }
+    if constexpr (mode != kModeOut)
+      nbad_w += (uint32_t)__builtin_popcountll(__ballot(pact && plast && li == 0u && !good));
     // The finishing group's result is parked in ONE lane of the group, the
     // lane whose index is the round number mod 8, and written by
     // flush_stores() once every 8 rounds: stores count in the same in-order
@@ -703,10 +726,7 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
     if (!(pact && plast)) return;
     const bool mine = li == (round & 7u);
     if constexpr (mode == kModeSstSeal) {  // table/table_builder.cc:245-249
-      if (!pfits) {
-        if (li == 0) nbad_l++;
-        return;
-      }
+      if (!pfits) return;
       const uint32_t typ = paux0 & 0xffu;
       const uint32_t m = mask_crc((l ^ advance_byte(typ)) ^ 0xffffffffu);  // Extend(crc, &type, 1)
       // the trailer [type][masked crc LE32] at pat, one byte per lane.  These
@@ -720,16 +740,12 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(li == 0 ? typ : m >> (8 * (li - 1)));
     } else if constexpr (mode == kModeSstCrc) {  // the same crc, dense: out[b]
       const uint32_t typ = paux0 & 0xffu;
-      if (!pfits && li == 0) nbad_l++;
       if (mine) {
         pend_a = reinterpret_cast<uint64_t>(args.out + pb);
         pend_v = pfits ? mask_crc((l ^ advance_byte(typ)) ^ 0xffffffffu) : 0u;
       }
     } else if constexpr (mode == kModeLogSeal) {  // log::Writer::EmitPhysicalRecord, common/log_writer.cc:85-88
-      if (!pfits && li == 0) {
-        if (args.out) args.out[pb] = 0;
-        nbad_l++;
-      }
+      if (!pfits && li == 0 && args.out) args.out[pb] = 0;
       if (pfits && mine) {  // header[0..4) at pat (+ out[pb] when requested)
         pend_a = pat;
         pend_v = mask_crc(crc);
@@ -740,16 +756,7 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
         pend_a = reinterpret_cast<uint64_t>(args.out + pb);
         pend_v = (args.flags & 1u) ? mask_crc(crc) : crc;
       }
-    } else {
-      bool good;
-      if constexpr (mode == kModeVerify)
-        good = ((args.flags & 1u) ? mask_crc(crc) : crc) == paux0;
-      else  // kModeSstVerify (table/format.cc:95-103), kModeLogVerify (log_reader.cc:228-242)
-#ifndef LSBM_VERIFY_TWO_LOADS
-        good = pfits && unmask_crc(paux0) == crc;
-#else
-        good = pfits && unmask_crc(unaligned_word(paux0, paux1, pat)) == crc;
-#endif
+    } else {  // verify modes: good (above)
 #ifdef LSBM_DIAG_VERIFY_WRITEBACK  // diagnostic builds only: rewrite the stored crc bytes
       if (pfits && li < 4)
         reinterpret_cast<uint8_t*>(pat)[li] = (uint8_t)(paux0 >> (8 * li));
@@ -758,7 +765,6 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
         pend_a = reinterpret_cast<uint64_t>(args.ok + pb);
         pend_v = good ? 1u : 0u;
       }
-      if (!good && li == 0) nbad_l++;
     }
   };
   auto flush_stores = [&]() {
@@ -1124,11 +1130,7 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
   }
   retire();
   flush_stores();
-  if (args.nbad) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) nbad_l += (uint32_t)__shfl_xor((int)nbad_l, (int)d);
-    if (lane == 0 && nbad_l) atomicAdd(args.nbad, nbad_l);
-  }
+  if (args.nbad && lane == 0 && nbad_w) atomicAdd(args.nbad, nbad_w);
 }
 
 }  // namespace lsbm

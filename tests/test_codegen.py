@@ -64,3 +64,29 @@ def test_snappy_decoder_m0_only_feeds_writelane(tmp_path):
                 assert in_asm, (sym, "M0 used outside the inline asm", line)
                 n_lane_m0 += line.startswith(("v_writelane_b32", "v_readlane_b32"))
         assert n_lane_m0 >= 1, (sym, "no lane select through M0 found")
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="hipcc not available")
+def test_crc_kernels_do_not_spill(tmp_path):
+    """The fixed-stride and units kernels keep everything in registers (round 6:
+    one extra per-lane counter made the SSTable walks spill 12-20 bytes to
+    scratch, and SSTable verify / trailer CRCs / seal lost 1.3-2.5 points of
+    HBM peak against round 5's build on the same box, profiles/r06/events_ab/).
+    A scratch access in the round loop sits in the same in-order vmcnt queue as
+    the row loads."""
+    src = os.path.join(REPO, "lsbm_amd", "csrc", "crc32c_kernels.hip")
+    s_file = tmp_path / "crc32c_kernels.s"
+    subprocess.run([HIPCC if os.path.exists(HIPCC) else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-w", "-I", os.path.join(REPO, "include"), "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+                    "--cuda-device-only", "-S", "-o", str(s_file), src], check=True, timeout=900)
+    scratch, name = {}, None
+    for line in s_file.read_text().splitlines():
+        m = re.match(r"^(_Z\w+):", line)
+        if m:
+            name = m.group(1)
+        m = re.match(r"^; ScratchSize: (\d+)", line)
+        if m and name:
+            scratch[name] = int(m.group(1))
+    crc = {k: v for k, v in scratch.items() if "crc32c_fixed_kernel" in k or "crc32c_units_kernel" in k}
+    assert len(crc) >= 10, sorted(scratch)
+    assert not {k: v for k, v in crc.items() if v}, crc

@@ -107,7 +107,7 @@ def sst(entry, reps):
         t = time_launches(lambda: engine.crc32c_extents(d, ext, out=out, stream=s), s, reps=reps)
         got = out.cpu().numpy().view(np.uint32)
         bad = sum(int(got[b] != o.value(stream_bytes(0x5EED0005, int(offs[b]), L + 1).tobytes())) for b in sample)
-        return line(entry, r"crc32c_units_kernel<48u, 0u, 1u>", n * (L + 1), t, bad, blocks=n)
+        return line(entry, r"crc32c_units_kernel<48u, 0u, 1u, ", n * (L + 1), t, bad, blocks=n)
     # seal first (the other entries read its trailers), untimed when it is not the entry
     if entry == "sst_seal":
         t = time_launches(lambda: table.seal_blocks(d, handles, types, stream=s), s, reps=reps)
@@ -120,18 +120,18 @@ def sst(entry, reps):
               (img[ends + 3].astype(np.uint32) << 16) | (img[ends + 4].astype(np.uint32) << 24))
     bad = sum(int(stored[b] != o.mask(o.value(img[offs[b]:offs[b] + L + 1].tobytes()))) for b in sample)
     if entry == "sst_seal":
-        return line(entry, r"crc32c_units_kernel<40u, 6u, 1u>", n * (L + 1), t, bad, blocks=n)
+        return line(entry, r"crc32c_units_kernel<40u, 6u, 1u, ", n * (L + 1), t, bad, blocks=n)
     if entry == "sst_crcs":
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         nb = torch.zeros(1, dtype=torch.int32, device="cuda")
         t = time_launches(lambda: table.trailer_crcs(d, handles, types, stream=s, out=out, nbad=nb), s, reps=reps)
         bad += int(not np.array_equal(out.cpu().numpy().view(np.uint32), stored))
-        return line(entry, r"crc32c_units_kernel<40u, 6u, 1u>", n * (L + 1), t, bad, blocks=n)
+        return line(entry, r"crc32c_units_kernel<40u, 6u, 1u, ", n * (L + 1), t, bad, blocks=n)
     if entry == "sst_verify":
         t = time_launches(lambda: table.verify_blocks(d, handles, stream=s), s, reps=reps)
         ok, nbad = table.verify_blocks(d, handles, stream=s)
         bad += int(not bool(ok.all().item()) or int(nbad.item()) != 0)
-        return line(entry, r"crc32c_units_kernel<40u, 3u, 1u>", n * (L + 1), t, bad, blocks=n)
+        return line(entry, r"crc32c_units_kernel<40u, 3u, 1u, ", n * (L + 1), t, bad, blocks=n)
     raise SystemExit(f"unknown entry {entry}")
 
 
