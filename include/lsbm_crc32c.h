@@ -213,7 +213,7 @@ int lsbm_test_ragged_kernel(int which);
 int lsbm_test_fixed_queue(int on);
 /* Testing / A/B: SSTable trailer batches (verify, dense trailer CRCs) as
  * equal-count pieces claimed by a workgroup's waves (1) or one range per wave
- * (0); -1 restores the default (LSBM_SST_PIECES, pieces). */
+ * (0); -1 restores the default (LSBM_SST_PIECES, one range per wave). */
 int lsbm_test_sst_pieces(int on);
 
 /* ---- host runtime (the C++ layers' sessions and worker pool) ---- */

@@ -251,14 +251,16 @@ bool fixed_queue_on() {
   return q == 1;
 }
 
-// SSTable trailer batches as claimed equal-count pieces (default) or one range
-// per wave (LSBM_SST_PIECES=0, lsbm_test_sst_pieces: A/B runs).
+// SSTable trailer batches as claimed equal-count pieces (LSBM_SST_PIECES=1,
+// lsbm_test_sst_pieces: A/B runs) or one range per wave (the default: in one
+// process over one image, pieces ran 0.1-0.35 points slower, round 6,
+// profiles/r06/events_ab/sst_pieces_inproc.log).
 std::atomic<int> g_sst_pieces{-1};  // -1: not read yet
 bool sst_pieces_on() {
   int q = g_sst_pieces.load(std::memory_order_relaxed);
   if (q < 0) {
     const char* v = getenv("LSBM_SST_PIECES");
-    q = (v && v[0] == '0') ? 0 : 1;
+    q = (v && v[0] == '1') ? 1 : 0;
     int expect = -1;
     if (!g_sst_pieces.compare_exchange_strong(expect, q)) q = expect;
   }

@@ -1272,14 +1272,25 @@ def test_host_staged_multi_device_shards(torch_cuda, oracle):
         assert np.array_equal(got, oracle.batch_offsets(data, offs, init, masked=True)), devs
 
 
+@pytest.mark.parametrize("pieces", [0, 1])
 @pytest.mark.parametrize("order", ["sorted", "shuffled"])
-def test_sst_claimed_pieces_ragged_sizes(torch_cuda, oracle, order):
-    """SSTable verify and dense trailer CRCs over >= 131,072 handles go as
-    equal-count pieces claimed in turn by a workgroup's waves (crc32c_units.h
-    next_piece; round 6).  Here 300,001 blocks of 0-9,000 B (so the pieces are
-    far from equal in bytes), handles in file order or shuffled, a few past
-    the image: every trailer CRC equals the oracle's WriteRawBlock CRC, every
-    verify flag is right, and the bad handles are counted exactly."""
+def test_sst_claimed_pieces_ragged_sizes(torch_cuda, oracle, product_lib, order, pieces):
+    """SSTable verify and dense trailer CRCs over >= 131,072 handles, under
+    both schedules: one range per wave (the default) and equal-count pieces
+    claimed in turn by a workgroup's waves (lsbm_test_sst_pieces(1),
+    crc32c_units.h next_piece; round 6).  Here 300,001 blocks of 0-9,000 B
+    (so the pieces are far from equal in bytes), handles in file order or
+    shuffled, a few past the image: every trailer CRC equals the oracle's
+    WriteRawBlock CRC, every verify flag is right, and the bad handles are
+    counted exactly."""
+    assert product_lib.lsbm_test_sst_pieces(pieces) == 0
+    try:
+        _sst_ragged_sizes(torch_cuda, oracle, order)
+    finally:
+        product_lib.lsbm_test_sst_pieces(-1)
+
+
+def _sst_ragged_sizes(torch_cuda, oracle, order):
     torch = torch_cuda
     from lsbm_amd import table
     rng = np.random.default_rng(21)
@@ -1306,10 +1317,10 @@ def test_sst_claimed_pieces_ragged_sizes(torch_cuda, oracle, order):
     assert int(nb.item()) == len(bad)
     assert np.array_equal(_u32(tc), want)
     # the image is not sealed yet: every block fails verify (and is counted:
-    # per lane, one atomic per walk)
+    # one ballot per round, one atomic per walk)
     ok, nb = table.verify_blocks(d, dh)
     assert int(nb.item()) == n and not bool(ok.any())
-    # seal (the fused seal, static ranges) then verify (claimed pieces)
+    # seal (the fused seal, one range per wave) then verify
     nbad = table.seal_blocks(d, dh, _dev(torch, t2))
     assert int(nbad.item()) == len(bad)
     ok, nb = table.verify_blocks(d, dh)
