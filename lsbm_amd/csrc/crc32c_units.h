@@ -554,6 +554,14 @@ __device__ __forceinline__ uint32_t next_piece(lds_u32* claim, uint32_t pi, uint
   return pi + (uint32_t)nwaves;
 }
 
+// Rows of a round the walk absorbs at raised wave priority (units_walk;
+// 8, 12, 16, ...: the row loop's bank boundaries).
+#ifndef LSBM_PRIO_ROWS  // (A/B builds override)
+#define LSBM_PRIO_ROWS 8
+#endif
+constexpr uint32_t kPrioRows = LSBM_PRIO_ROWS;
+static_assert(kPrioRows >= 8 && kPrioRows % 4 == 0, "priority lowered at a bank boundary of the row loop");
+
 // The units walk: the blocks [b_lo, b_hi) (or, chunked, this wave's range of
 // every chunk) in rounds of 8 units.  crc32c_units_kernel runs it over the
 // wave's range; crc32c_stream_kernel runs it over a sub-piece whose extents
@@ -805,6 +813,15 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
   };
 
   while (cur_b < range_hi) {
+    // The round's prologue at raised wave priority (round 6): from the end of
+    // the last round's rows to this round's first row loads the wave has no
+    // row loads in flight, while the other waves of its SIMD stream at normal
+    // priority; at s_setprio 2 it takes the issue slots until it has absorbed
+    // this round's first kPrioRows rows.  A/B, same box: SSTable verify /
+    // trailer CRCs / seal +1.5-1.9 points of HBM peak (priority only until the
+    // first loads: +0.2-0.4); the fixed kernel, whose group prologue is
+    // short, unchanged (profiles/r06/events_ab/prio_*.log).
+    __builtin_amdgcn_s_setprio(2);
     // Find the 8 groups' units in one round: lane j holds block cur_b + j
     // (8 units never span more than 9 blocks), an inclusive prefix sum over
     // the lanes' unit counts, then one ballot per group.  ALU + shuffles only:
@@ -1064,12 +1081,15 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
       for (uint32_t k2 = 0; k2 < 4; k2++) ba[k2] = __builtin_nontemporal_load(row_addr(r + 4 + k2));
 #pragma unroll
       for (uint32_t k2 = 0; k2 < 4; k2++) absorb(bb[k2], r + k2);
+      if (r + 4 == kPrioRows) __builtin_amdgcn_s_setprio(0);
       if (r + 4 >= rows_max) break;
 #pragma unroll
       for (uint32_t k2 = 0; k2 < 4; k2++) bb[k2] = __builtin_nontemporal_load(row_addr(r + 8 + k2));
 #pragma unroll
       for (uint32_t k2 = 0; k2 < 4; k2++) absorb(ba[k2], r + 4 + k2);
+      if (r + 8 == kPrioRows) __builtin_amdgcn_s_setprio(0);
     }
+    __builtin_amdgcn_s_setprio(0);  // (a round of fewer rows)
     c0 ^= dx;
     c1 ^= dy;
     c2 ^= dz;
