@@ -557,7 +557,7 @@ __device__ __forceinline__ uint32_t next_piece(lds_u32* claim, uint32_t pi, uint
 // Rows of a round the walk absorbs at raised wave priority (units_walk;
 // 8, 12, 16, ...: the row loop's bank boundaries).
 #ifndef LSBM_PRIO_ROWS  // (A/B builds override)
-#define LSBM_PRIO_ROWS 8
+#define LSBM_PRIO_ROWS 16
 #endif
 constexpr uint32_t kPrioRows = LSBM_PRIO_ROWS;
 static_assert(kPrioRows >= 8 && kPrioRows % 4 == 0, "priority lowered at a bank boundary of the row loop");
@@ -818,9 +818,10 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
     // row loads in flight, while the other waves of its SIMD stream at normal
     // priority; at s_setprio 2 it takes the issue slots until it has absorbed
     // this round's first kPrioRows rows.  A/B, same box: SSTable verify /
-    // trailer CRCs / seal +1.5-1.9 points of HBM peak (priority only until the
-    // first loads: +0.2-0.4); the fixed kernel, whose group prologue is
-    // short, unchanged (profiles/r06/events_ab/prio_*.log).
+    // trailer CRCs / seal +2-2.5 points of HBM peak at 16 rows (8: +1.5-1.9;
+    // only until the first loads: +0.2-0.4); the fixed kernel, whose group
+    // prologue is short, and the stream kernel's sub-piece set-up or tail
+    // (config 4 -0.7 to -2) gain nothing (profiles/r06/events_ab/prio_*.log).
     __builtin_amdgcn_s_setprio(2);
     // Find the 8 groups' units in one round: lane j holds block cur_b + j
     // (8 units never span more than 9 blocks), an inclusive prefix sum over
