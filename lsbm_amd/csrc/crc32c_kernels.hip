@@ -230,16 +230,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_fixed_kernel(
 // kernel 13 points of HBM bandwidth when done in it, and a separate pass of
 // byte stores as much again (0.17 ms); the compare-and-swap pass, ~0.03 ms.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void cas_merge_from(unsigned long long* p, uint64_t m, uint64_t v,
-                                               unsigned long long old) {
-  for (;;) {
-    const unsigned long long want = (old & ~m) | (v & m);
-    if (want == old) return;
-    const unsigned long long got = atomicCAS(p, old, want);
-    if (got == old) return;
-    old = got;
-  }
-}
 __device__ __forceinline__ void cas_merge(unsigned long long* p, uint64_t m, uint64_t v) {
   unsigned long long old = *p;
   for (;;) {
@@ -265,67 +255,6 @@ __device__ __forceinline__ void merge_bytes(uint64_t img, uint64_t limit, uint64
   unsigned long long* w = reinterpret_cast<unsigned long long*>(w0a);
   cas_merge(w, fm << (8 * sh), v << (8 * sh));
   if (two) cas_merge(w + 1, fm >> (64 - 8 * sh), v >> (64 - 8 * sh));
-}
-
-// The fused seal's epilogue (crc32c_units_kernel, SstCrc with args.file): the
-// trailers of this wave's blocks [b_lo, b_hi), kSealU blocks per lane at a
-// time, each step issued for all of them before any waits -- the handles,
-// types and CRCs; the image words around each trailer; the compare-and-swaps
-// (retried only where a swap lost) -- so three memory latencies per kSealU
-// blocks instead of three per block: the last waves' merges end the launch.
-constexpr uint32_t kSealU = 4;
-__device__ __forceinline__ void seal_epilogue(const RaggedArgs& args, uint64_t b_lo, uint64_t b_hi) {
-  const uint64_t img = reinterpret_cast<uint64_t>(args.file), limit = args.limit;
-  const uint32_t lane = threadIdx.x & 63u;
-  constexpr uint64_t fm = (1ull << 40) - 1;  // the 5 trailer bytes
-  for (uint64_t i0 = b_lo; i0 < b_hi; i0 += 64ull * kSealU) {
-    uint64_t t[kSealU], v[kSealU];
-    bool go[kSealU];
-#pragma unroll
-    for (uint32_t u = 0; u < kSealU; u++) {
-      const uint64_t i = i0 + 64ull * u + lane;
-      const bool in = i < b_hi;
-      const uint64_t j = in ? i : b_lo;  // (clamped: the loads are unconditional)
-      const uint64_t off = args.handles[2 * j], size = args.handles[2 * j + 1];
-      const uint32_t crc = __hip_atomic_load(args.out + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t typ = args.types[j];
-      go[u] = in && off <= limit && limit - off >= kTrailer && limit - off - kTrailer >= size;
-      t[u] = img + off + size;
-      v[u] = typ | ((uint64_t)crc << 8);
-    }
-    unsigned long long o0[kSealU], o1[kSealU];
-#pragma unroll
-    for (uint32_t u = 0; u < kSealU; u++) {  // the words' current values (plain loads: guesses the swaps check)
-      const uint64_t w0a = t[u] & ~7ull;
-      const bool two = (t[u] & 7u) + kTrailer > 8u;
-      const bool words = go[u] && w0a >= img && w0a + (two ? 16u : 8u) <= img + limit;
-      o0[u] = words ? *reinterpret_cast<const unsigned long long*>(w0a) : 0ull;
-      o1[u] = words && two ? *reinterpret_cast<const unsigned long long*>(w0a + 8u) : 0ull;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kSealU; u++) {
-      if (!go[u]) continue;
-      const uint32_t sh = (uint32_t)(t[u] & 7u);
-      const uint64_t w0a = t[u] & ~7ull;
-      const bool two = sh + kTrailer > 8u;
-      if (w0a < img || w0a + (two ? 16u : 8u) > img + limit) {  // words reaching outside the image: bytes
-        merge_bytes(img, limit, t[u], kTrailer, v[u]);
-        continue;
-      }
-      unsigned long long* w = reinterpret_cast<unsigned long long*>(w0a);
-      const uint64_t m0 = fm << (8 * sh), m1 = two ? fm >> (64 - 8 * sh) : 0ull;
-      const uint64_t x0 = v[u] << (8 * sh), x1 = two ? v[u] >> (64 - 8 * sh) : 0ull;
-      const unsigned long long want0 = (o0[u] & ~m0) | (x0 & m0);
-      const unsigned long long g0 = want0 != o0[u] ? atomicCAS(w, o0[u], want0) : o0[u];
-      unsigned long long g1 = o1[u];
-      if (two) {
-        const unsigned long long want1 = (o1[u] & ~m1) | (x1 & m1);
-        g1 = want1 != o1[u] ? atomicCAS(w + 1, o1[u], want1) : o1[u];
-      }
-      if (g0 != o0[u]) cas_merge_from(w, m0, x0, g0);  // (lost a race or a stale guess: again from there)
-      if (two && g1 != o1[u]) cas_merge_from(w + 1, m1, x1, g1);
-    }
-  }
 }
 
 __global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ file, uint64_t limit,
@@ -384,7 +313,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_units_kernel(RaggedArgs 
       // this wave's out[] stores complete (s_waitcnt vmcnt(0)) before it reads
       // them back past L1 (an agent-scope fence would write back the whole L2)
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      seal_epilogue(args, b_lo, b_hi);
+      const uint64_t img = reinterpret_cast<uint64_t>(args.file), limit = args.limit;
+      const uint32_t lane = threadIdx.x & 63u;
+      for (uint64_t i = b_lo + lane; i < b_hi; i += 64) {
+        const uint64_t off = args.handles[2 * i], size = args.handles[2 * i + 1];
+        if (!(off <= limit && limit - off >= kTrailer && limit - off - kTrailer >= size)) continue;
+        const uint32_t crc = __hip_atomic_load(args.out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        merge_bytes(img, limit, img + off + size, 5, (uint64_t)args.types[i] | ((uint64_t)crc << 8));
+      }
     }
   }
   DIAG_STAMP(2);
