@@ -819,7 +819,8 @@ __device__ __forceinline__ void units_walk(RaggedArgs args, const uint64_t wave,
     // priority; at s_setprio 2 it takes the issue slots until it has absorbed
     // this round's first kPrioRows rows.  A/B, same box: SSTable verify /
     // trailer CRCs / seal +2-2.5 points of HBM peak at 16 rows (8: +1.5-1.9;
-    // only until the first loads: +0.2-0.4); the fixed kernel, whose group
+    // 24: 0.2-0.4 less; 32, near a whole round: 1.5 less; only until the
+    // first loads: +0.2-0.4); the fixed kernel, whose group
     // prologue is short, and the stream kernel's sub-piece set-up or tail
     // (config 4 -0.7 to -2) gain nothing (profiles/r06/events_ab/prio_*.log).
     __builtin_amdgcn_s_setprio(2);
